@@ -1,0 +1,82 @@
+"""Synthetic workloads shared by the parity tests, the golden-vector generator and bench.py.
+
+SURVEY.md §8(d) restates BASELINE.json's metric as synthetic inputs:
+
+* stream ``s`` carries a payload from ``np.random.default_rng([20251010, s])``; bits are LSB-first per
+  byte, the convention of ``src/neuralstego/api.py:153-157`` and ``lm/arithmetic.py:30-35``;
+* context = ``[50256] + list(range(1000, 1031))``;
+* coder-only logits: row ``(s, t)`` = ``scale * N(0, 1)`` drawn from ``default_rng([seed, s, t])``.
+
+Nothing here touches the GPU; callers copy the arrays where they need them.
+"""
+
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+
+PAYLOAD_SEED = 20251010
+DEFAULT_CONTEXT: List[int] = [50256] + list(range(1000, 1031))
+GPT2_VOCAB = 50257
+
+
+def payload_bytes(stream: int, nbytes: int, seed: int = PAYLOAD_SEED) -> bytes:
+    """Random payload of stream ``stream``."""
+    return np.random.default_rng([seed, stream]).bytes(nbytes)
+
+
+def bytes_to_bits_lsb(data: bytes) -> List[int]:
+    """LSB-first bit list, as ``src/neuralstego/api.py:153-157`` builds it."""
+    arr = np.frombuffer(bytes(data), dtype=np.uint8)
+    return np.unpackbits(arr, bitorder="little").astype(np.int64).tolist()
+
+
+def bits_to_bytes_lsb(bits: Sequence[int]) -> bytes:
+    """Inverse of :func:`bytes_to_bits_lsb` (``api.py:160-170``); pads the last byte with zeros."""
+    arr = np.asarray(list(bits), dtype=np.uint8)
+    return np.packbits(arr, bitorder="little").tobytes()
+
+
+def pack_bits_lsb(bits: Sequence[int]) -> np.ndarray:
+    """Pack a bit list into the coder's payload byte layout: bit ``j`` is ``byte[j >> 3] >> (j & 7)``."""
+    arr = np.asarray(list(bits), dtype=np.uint8)
+    if arr.size == 0:
+        return np.zeros(0, dtype=np.uint8)
+    return np.packbits(arr, bitorder="little")
+
+
+def unpack_bits_lsb(packed: np.ndarray, nbits: int) -> List[int]:
+    bits = np.unpackbits(np.asarray(packed, dtype=np.uint8), bitorder="little")
+    return bits[:nbits].astype(np.int64).tolist()
+
+
+def logits_row(seed: int, stream: int, step: int, vocab: int, scale: float = 3.0,
+               dtype=np.float32) -> np.ndarray:
+    """One synthetic logit row; the same generator feeds the HIP kernel and the CPU oracle."""
+    rng = np.random.default_rng([seed, stream, step])
+    return (scale * rng.standard_normal(vocab)).astype(np.float32).astype(dtype)
+
+
+def logits_batch(seed: int, streams: Sequence[int], step: int, vocab: int, scale: float = 3.0,
+                 dtype=np.float32, ld: int | None = None) -> np.ndarray:
+    """``[len(streams), ld]`` batch of rows; columns ``[vocab, ld)`` are zero padding."""
+    ld = vocab if ld is None else ld
+    out = np.zeros((len(streams), ld), dtype=dtype)
+    for r, s in enumerate(streams):
+        out[r, :vocab] = logits_row(seed, s, step, vocab, scale, dtype)
+    return out
+
+
+def top_region_tie_free(row: np.ndarray, topk: int, banned: Sequence[int]) -> bool:
+    """True when the ``topk + 1`` largest non-banned values are pairwise distinct.
+
+    The reference sorts with ``torch.sort(descending=True)`` (``code_base/arithmetic.py:127``), whose tie
+    order is unspecified; fixtures are generated with a stable sort and this check documents which rows
+    would be order-ambiguous under the unstable one.
+    """
+    vals = row.astype(np.float64).copy()
+    vals[list(banned)] = -np.inf
+    n = min(topk + 1, vals.size)
+    top = np.sort(vals)[::-1][:n]
+    return bool(np.all(top[:-1] != top[1:]))

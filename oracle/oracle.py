@@ -1,0 +1,168 @@
+"""ctypes front end of the CPU oracle (``oracle/nsg_oracle.c``).  TEST INFRASTRUCTURE ONLY.
+
+Imported only by ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg, always as
+the checker or the timed CPU baseline, never as the thing measured or shipped.
+
+The per-stream loops below restate the reference drivers: ``encode_stream`` is the
+``while i < len(message)`` loop of ``code_base/arithmetic.py:112-210`` and ``decode_stream`` the
+``while i < len(inp)`` loop of ``code_base/arithmetic.py:254-371`` (without the BPE-repair heuristics of
+``:300-342``: a received token outside the kept top-k is reported as a divergence).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+from typing import Callable, List, Sequence, Tuple
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "libnsgoracle.so"
+
+OR_OK, OR_ERR_CONFIG, OR_ERR_RANGE, OR_ERR_DIVERGE = 0, -1, -2, -3
+
+
+class OrState(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64), ("bit_pos", ctypes.c_int64),
+                ("ntokens", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class OrTrace(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("kprime", ctypes.c_int32), ("sel", ctypes.c_int32),
+                ("n", ctypes.c_int32), ("token", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("S", ctypes.c_double)]
+
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = ctypes.CDLL(str(LIB_PATH))
+        fp = ctypes.POINTER(ctypes.c_float)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.or_exp_canon.restype = ctypes.c_double
+        L.or_exp_canon.argtypes = [ctypes.c_double]
+        L.or_select_cutoff_k.restype = ctypes.c_int
+        L.or_select_cutoff_k.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_double,
+                                         ctypes.c_int]
+        L.or_init_state.argtypes = [ctypes.POINTER(OrState), ctypes.c_int]
+        L.or_encode_step.restype = ctypes.c_int
+        L.or_encode_step.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                     ctypes.c_int, u8p, ctypes.c_int64, ctypes.POINTER(OrState), i32p,
+                                     ctypes.POINTER(OrTrace)]
+        L.or_decode_step.restype = ctypes.c_int
+        L.or_decode_step.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int32, ctypes.c_int, ctypes.POINTER(OrState), u8p,
+                                     ctypes.POINTER(OrTrace)]
+        L.or_row_sum.restype = ctypes.c_double
+        L.or_row_sum.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.or_encode_batch.restype = ctypes.c_int
+        L.or_encode_batch.argtypes = [fp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, i32p, ctypes.c_int,
+                                      ctypes.c_double, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int64,
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(OrState), i32p]
+        _lib = L
+    return _lib
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _i32(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def exp_canon(d: float) -> float:
+    return lib().or_exp_canon(float(d))
+
+
+def select_cutoff_k(probs: Sequence[float], threshold: float, topk: int) -> int:
+    p = np.ascontiguousarray(probs, dtype=np.float64)
+    return lib().or_select_cutoff_k(p.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), p.size,
+                                   float(threshold), int(topk))
+
+
+def new_state(precision: int) -> OrState:
+    st = OrState()
+    lib().or_init_state(ctypes.byref(st), int(precision))
+    return st
+
+
+def encode_step(row: np.ndarray, st: OrState, payload: np.ndarray, nbits: int, *, banned, temp: float,
+                precision: int, topk: int) -> Tuple[int, int, OrTrace]:
+    x = np.ascontiguousarray(row, dtype=np.float32)
+    b = np.ascontiguousarray(banned, dtype=np.int32)
+    pl = np.ascontiguousarray(payload, dtype=np.uint8)
+    if pl.size == 0:
+        pl = np.zeros(1, np.uint8)
+    tok = ctypes.c_int32(-1)
+    tr = OrTrace()
+    rc = lib().or_encode_step(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(precision), int(topk),
+                              _u8(pl), int(nbits), ctypes.byref(st), ctypes.byref(tok), ctypes.byref(tr))
+    return rc, tok.value, tr
+
+
+def decode_step(row: np.ndarray, st: OrState, token: int, is_last: bool, out_bits: np.ndarray, *, banned,
+                temp: float, precision: int, topk: int) -> Tuple[int, OrTrace]:
+    x = np.ascontiguousarray(row, dtype=np.float32)
+    b = np.ascontiguousarray(banned, dtype=np.int32)
+    tr = OrTrace()
+    rc = lib().or_decode_step(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(precision), int(topk),
+                              int(token), int(bool(is_last)), ctypes.byref(st), _u8(out_bits), ctypes.byref(tr))
+    return rc, tr
+
+
+RowFn = Callable[[int], np.ndarray]
+
+
+def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, precision: int, topk: int,
+                  max_steps: int = 1 << 20) -> Tuple[List[int], List[OrTrace]]:
+    """Encode one bit list (``code_base/arithmetic.py:112-210`` loop); ``row_fn(t)`` gives step t's logits."""
+    nbits = len(bits)
+    packed = np.packbits(np.asarray(bits, dtype=np.uint8), bitorder="little") if nbits else np.zeros(1, np.uint8)
+    st = new_state(precision)
+    toks, traces = [], []
+    t = 0
+    while st.bit_pos < nbits:
+        if t >= max_steps:
+            raise RuntimeError("oracle encode did not terminate")
+        rc, tok, tr = encode_step(row_fn(t), st, packed, nbits, banned=banned, temp=temp, precision=precision,
+                                  topk=topk)
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle encode step {t} failed rc={rc}")
+        toks.append(tok)
+        traces.append(tr)
+        t += 1
+    return toks, traces
+
+
+def decode_stream(row_fn: RowFn, tokens: Sequence[int], *, banned, temp: float, precision: int,
+                  topk: int) -> Tuple[List[int], List[OrTrace]]:
+    """Decode a token list (``code_base/arithmetic.py:254-371`` loop) into the full emitted bit list."""
+    st = new_state(precision)
+    out = np.zeros((len(tokens) * max(precision, 1) + 7) // 8 + 8, dtype=np.uint8)
+    traces = []
+    for t, tok in enumerate(tokens):
+        rc, tr = decode_step(row_fn(t), st, int(tok), t == len(tokens) - 1, out, banned=banned, temp=temp,
+                             precision=precision, topk=topk)
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle decode step {t} failed rc={rc}")
+        traces.append(tr)
+    bits = np.unpackbits(out, bitorder="little")[: st.bit_pos].astype(np.int64).tolist()
+    return bits, traces

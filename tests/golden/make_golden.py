@@ -1,0 +1,179 @@
+"""Generate golden vectors by running the REFERENCE coder (``code_base/arithmetic.py``) in this container.
+
+This script is the only place that executes reference code. It runs here (the build container, where
+``/root/reference`` is mounted) and writes small ``.npz`` fixtures next to itself; the fixtures are data
+(inputs + the reference's outputs) and travel with the repo. Nothing on the GPU box reads
+``/root/reference``.
+
+Shims:
+
+* ``sys.modules["bitarray"]`` = stub (``code_base/utils.py:3`` imports it; the coder never uses it);
+* ``code_base/`` first on ``sys.path`` (``arithmetic.py:9`` does ``from utils import ...``);
+* ``arithmetic.max_positions = 1024`` (decode reads an undefined global, ``arithmetic.py:257``);
+* the model is a synthetic-logit callable returning ``.logits [1, T, V]`` and ``.past_key_values=None``
+  (so ``_prepare_past_for_model``/``_normalise_past`` see ``None`` and no transformers cache API runs);
+* the tokenizer stub's ``decode`` never yields ``'<eos>'`` (``arithmetic.py:208-210``) and its ``encode``
+  returns the preset token list (``arithmetic.py:233``);
+* ``torch.Tensor.sort`` is forced ``stable=True`` through a ``TorchFunctionMode``: the reference's
+  ``sort(descending=True)`` (``arithmetic.py:127,268``) has unspecified tie order; the stable order
+  (value desc, token id asc) is the build's canonical tie-break (SURVEY.md §7 hard part 2).
+
+Usage: ``python tests/golden/make_golden.py`` (about a minute on 8 cores).
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+import time
+import types
+from pathlib import Path
+
+import numpy as np
+
+REF = Path("/root/reference")
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parents[1]
+sys.path.insert(0, str(REPO))
+
+from neuralsteganography_amd import synthetic  # noqa: E402
+
+
+def _import_reference():
+    import torch
+    from torch.overrides import TorchFunctionMode
+
+    sys.modules.setdefault("bitarray", types.ModuleType("bitarray"))
+    sys.path.insert(0, str(REF / "code_base"))
+    import arithmetic as ref  # code_base/arithmetic.py
+
+    assert Path(ref.__file__).resolve() == (REF / "code_base" / "arithmetic.py").resolve(), ref.__file__
+    ref.max_positions = 1024
+
+    class StableSort(TorchFunctionMode):
+        def __torch_function__(self, func, types_, args=(), kwargs=None):
+            kwargs = dict(kwargs or {})
+            if func in (torch.Tensor.sort, torch.sort):
+                kwargs["stable"] = True
+            return func(*args, **kwargs)
+
+    return ref, StableSort
+
+
+class SyntheticModel:
+    """Synthetic LM: call ``t`` returns row ``logits_row(seed, stream, t)`` (context is ignored)."""
+
+    def __init__(self, seed, stream, vocab, scale, dtype):
+        import torch
+
+        self.torch = torch
+        self.seed, self.stream, self.vocab, self.scale, self.dtype = seed, stream, vocab, scale, dtype
+        self.calls = 0
+        self.config = types.SimpleNamespace(n_positions=1024)
+
+    def __call__(self, input_ids, past_key_values=None, use_cache=True, position_ids=None):
+        row = synthetic.logits_row(self.seed, self.stream, self.calls, self.vocab, self.scale, self.dtype)
+        self.calls += 1
+        T = int(input_ids.shape[-1])
+        logits = self.torch.zeros((1, T, self.vocab), dtype=self.torch.from_numpy(row).dtype)
+        logits[0, -1] = self.torch.from_numpy(row.copy())
+        return types.SimpleNamespace(logits=logits, past_key_values=None)
+
+
+class StubTokenizer:
+    def __init__(self, tokens=None):
+        self.tokens = list(tokens or [])
+
+    def decode(self, ids):
+        return ""
+
+    def encode(self, text):
+        return list(self.tokens)
+
+
+CONFIGS = {
+    # name: vocab, dtype, logit scale, temp, precision, topk, payload bit lengths per stream
+    # C2-C4 coder parameters (code_base/run_single.py:21-24) on V = 50,257.
+    "g1_v50257_f32_p26_k300": dict(vocab=50257, dtype="f32", scale=3.0, temp=0.9, precision=26, topk=300,
+                                   nbits=[384, 384, 256, 1, 7, 13, 200, 512]),
+    # C5-like: fp16 logits (ties are common), topk 100.
+    "g2_v50257_f16_p26_k100": dict(vocab=50257, dtype="f16", scale=3.0, temp=0.9, precision=26, topk=100,
+                                   nbits=[256, 256, 128, 64]),
+    # Peaked rows (scale 10): the 1/R threshold binds, so k < topk on many steps.
+    "g3_v50257_f32_peaked_p26_k300": dict(vocab=50257, dtype="f32", scale=10.0, temp=1.0, precision=26,
+                                          topk=300, nbits=[256, 256, 128, 64]),
+    # api.py defaults (_DEFAULT_QUALITY, api.py:81-86): precision 16, topk 50000 (k in the thousands).
+    "g4_v50257_f32_p16_k50000": dict(vocab=50257, dtype="f32", scale=3.0, temp=1.0, precision=16,
+                                     topk=50000, nbits=[128, 96]),
+    # message->bits mode (code_base/run_single.py:52-54): precision 40, topk 60000.
+    "g5_v50257_f32_p40_k60000": dict(vocab=50257, dtype="f32", scale=3.0, temp=0.9, precision=40,
+                                     topk=60000, nbits=[96, 64]),
+    # Small vocabulary (still > 628, the reference bans id 628 unconditionally).
+    "g6_v700_f32_p20_k500": dict(vocab=700, dtype="f32", scale=2.0, temp=0.8, precision=20, topk=500,
+                                 nbits=[256, 100, 33, 8]),
+    # topk above the non-banned count: every candidate kept.
+    "g7_v640_f32_p12_k1000": dict(vocab=640, dtype="f32", scale=1.0, temp=1.3, precision=12, topk=1000,
+                                  nbits=[200, 64]),
+}
+
+LOGIT_SEED = 7
+
+
+def run_config(name, cfg, ref, stable_sort_mode):
+    dtype = np.float16 if cfg["dtype"] == "f16" else np.float32
+    V = cfg["vocab"]
+    banned = [V - 1, 628]
+    context = synthetic.DEFAULT_CONTEXT
+    out = {"tokens": [], "tok_off": [0], "bits": [], "bit_off": [0], "msg": [], "msg_off": [0],
+           "stats": [], "tie_free": []}
+    for s, nbits in enumerate(cfg["nbits"]):
+        nbytes = (nbits + 7) // 8
+        msg = synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes))[:nbits]
+        model = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], dtype)
+        with stable_sort_mode():
+            toks, nll, kl_, wpb, hq = ref.encode_arithmetic(
+                model, StubTokenizer(), list(msg), context, device="cpu", temp=cfg["temp"],
+                precision=cfg["precision"], topk=cfg["topk"])
+        nsteps = model.calls
+        assert nsteps == len(toks)
+        dmodel = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], dtype)
+        with stable_sort_mode():
+            bits = ref.decode_arithmetic(dmodel, StubTokenizer(toks), "", context, device="cpu",
+                                         temp=cfg["temp"], precision=cfg["precision"], topk=cfg["topk"])
+        assert bits[:nbits] == msg, f"{name} stream {s}: reference round trip failed"
+        tie_free = all(synthetic.top_region_tie_free(
+            synthetic.logits_row(LOGIT_SEED, s, t, V, cfg["scale"], dtype), min(cfg["topk"], V), banned)
+            for t in range(nsteps))
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["bits"] += list(bits); out["bit_off"].append(len(out["bits"]))
+        out["msg"] += list(msg); out["msg_off"].append(len(out["msg"]))
+        out["stats"].append([nll, kl_, wpb, hq])
+        out["tie_free"].append(tie_free)
+        print(f"  {name} s={s} nbits={nbits} steps={nsteps} decoded={len(bits)} tie_free={tie_free}", flush=True)
+    return out
+
+
+def main(names=None):
+    ref, stable = _import_reference()
+    for name, cfg in CONFIGS.items():
+        if names and name not in names:
+            continue
+        t0 = time.time()
+        res = run_config(name, cfg, ref, stable)
+        meta = dict(cfg, name=name, logit_seed=LOGIT_SEED, payload_seed=synthetic.PAYLOAD_SEED,
+                    context=synthetic.DEFAULT_CONTEXT, banned=[cfg["vocab"] - 1, 628],
+                    reference="code_base/arithmetic.py encode_arithmetic/decode_arithmetic",
+                    sort="stable (value desc, id asc)")
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            bits=np.asarray(res["bits"], dtype=np.uint8), bit_off=np.asarray(res["bit_off"], np.int64),
+            msg=np.asarray(res["msg"], dtype=np.uint8), msg_off=np.asarray(res["msg_off"], np.int64),
+            stats=np.asarray(res["stats"], dtype=np.float64),
+            tie_free=np.asarray(res["tie_free"], dtype=np.bool_))
+        print(f"{name}: {time.time() - t0:.1f}s", flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
