@@ -1,0 +1,215 @@
+"""Benchmark of the batched arithmetic-coding hot path (BASELINE.json metric).
+
+Workload (config C3, one MI355X): B = 4096 independent streams, 1 KiB random payload each, GPT-2-small
+vocabulary V = 50,257, fp32 logits resident in HBM, temp 0.9, precision 26, topk 300, banned {V-1, 628}.
+A *step* is one coder step (top-k, float64 CDF, interval update, bit consume) over all B streams, i.e. one
+`ns_encode_step` launch over a [B, ld] logit matrix.  Logits come from a pool of distinct synthetic
+batches (3*N(0,1), far larger than the 256 MiB Infinity Cache) cycled step by step; each stream's payload
+cursor advances for real, so every step does new work.
+
+value = payload bits fixed per second over the whole job (sum over ranks); cover tokens/s is reported
+beside it.  Multi-GPU: one process per GPU, each with its own B streams (weak scaling, no collective on
+the data path).  Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--vocab", type=int, default=50257)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f16"])
+    ap.add_argument("--precision", type=int, default=26)
+    ap.add_argument("--topk", type=int, default=300)
+    ap.add_argument("--temp", type=float, default=0.9)
+    ap.add_argument("--payload-bytes", type=int, default=1024)
+    ap.add_argument("--pool", type=int, default=6, help="distinct logit batches cycled over the steps")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per launch measured by a rocprofv3 --pmc pass (corrected), if known")
+    return ap.parse_args()
+
+
+def cpu_baseline(pool_h, payload, nbits, args, seconds):
+    """The oracle port timed on one host core on a bounded sample of the same workload."""
+    from oracle import oracle
+    import ctypes
+
+    L = oracle.lib()
+    V, P = args.vocab, args.precision
+    rows_all = pool_h  # list of [Bs, ld] float32
+    Bs = rows_all[0].shape[0]
+    ld = rows_all[0].shape[1]
+    banned = np.asarray([V - 1, 628], dtype=np.int32)
+    st = (oracle.OrState * Bs)()
+    for i in range(Bs):
+        L.or_init_state(ctypes.byref(st[i]), P)
+    out = np.zeros(Bs, np.int32)
+    pl = np.ascontiguousarray(payload[:Bs])
+    nb = np.ascontiguousarray(nbits[:Bs])
+    steps = 0
+    bits0 = sum(st[i].bit_pos for i in range(Bs))
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        rows = np.ascontiguousarray(rows_all[steps % len(rows_all)])
+        rc = L.or_encode_batch(rows.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ld, Bs, V,
+                               banned.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 2, 1.0 / args.temp, P,
+                               args.topk, pl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), pl.shape[1],
+                               nb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), st,
+                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        assert rc == 0
+        steps += 1
+    dt = time.perf_counter() - t0
+    bits = sum(st[i].bit_pos for i in range(Bs)) - bits0
+    return {"value": bits / dt, "unit": "payload bits/s", "cores": 1, "kind": "port",
+            "cover_tokens_per_s": steps * Bs / dt,
+            "sample": f"oracle/nsg_oracle.c or_encode_batch, {Bs} streams x {steps} steps of the same logit pool "
+                      f"({dt:.1f} s on 1 core)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.coder import CoderContext, CoderParams, EncodeSession, row_stride
+
+    B, V = args.batch, args.vocab
+    params = CoderParams(vocab=V, precision=args.precision, temp=args.temp, topk=args.topk, dtype=args.dtype)
+    ctx = CoderContext(params, max_batch=B, device=dev.index)
+    ld = row_stride(V, args.dtype)
+    tdt = params.torch_dtype
+    gen = torch.Generator(device=dev)
+    pool = []
+    for i in range(args.pool):
+        gen.manual_seed(1000 * rank + i)
+        x = torch.randn((B, ld), generator=gen, device=dev, dtype=torch.float32).mul_(3.0)
+        pool.append(x.to(tdt))
+        del x
+    first = rank * B
+    payload_bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(first + s, args.payload_bytes))
+                    for s in range(B)]
+    sess = EncodeSession(ctx, payload_bits)
+    stream = torch.cuda.current_stream()
+
+    for t in range(args.warmup):
+        sess.step(pool[t % args.pool])
+    torch.cuda.synchronize()
+    f0 = sess.fields()
+    c0 = ctx.counters()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        ev[t][0].record(stream)
+        sess.step(pool[(args.warmup + t) % args.pool])
+        ev[t][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+
+    f1 = sess.fields()
+    c1 = ctx.counters()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    stream_steps = c1[0] - c0[0]
+    exact_steps = c1[1] - c0[1]
+    bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
+    sess.raise_errors()
+
+    tot = torch.tensor([float(bits), float(stream_steps), elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        s = tot[:2].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        mx = tot[2:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        bits_all, ss_all = float(s[0]), float(s[1])
+        elapsed_max, kern_ms_max = float(mx[0]), float(mx[1])
+    else:
+        bits_all, ss_all, elapsed_max, kern_ms_max = float(bits), float(stream_steps), elapsed, kern_ms
+
+    esz = 2 if args.dtype == "f16" else 4
+    per_stream_step = V * esz + 76  # logit row + state r/w (64) + token (4) + history (4) + payload window (~4)
+    alg_bytes = B * per_stream_step
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+
+    out = {
+        "metric": "payload bits/sec + cover tokens/sec, GPT-2 arithmetic stego at batch, 1-8 GPUs",
+        "value": bits_all / elapsed_max,
+        "unit": "payload bits/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"C3 coder hot path: {B} streams/GPU x 1 step of ns_encode_step on resident [{B},{ld}] "
+                        f"{args.dtype} logits (GPT-2-small vocab {V}), temp {args.temp}, precision "
+                        f"{args.precision}, topk {args.topk}, {args.payload_bytes}-byte payloads",
+            "global_batch": B * world, "vocab": V, "logits_dtype": args.dtype, "precision": args.precision,
+            "topk": args.topk, "temp": args.temp, "payload_bytes": args.payload_bytes, "logit_pool": args.pool,
+            "parallelism": f"dp{world} (independent streams, no collective)",
+        },
+        "cover_tokens_per_s": ss_all / elapsed_max,
+        "bits_per_token": bits_all / max(ss_all, 1.0),
+        "kernel_ms_avg": kern_ms,
+        "exact_sum_fraction": exact_steps / max(stream_steps, 1),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": args.traffic_bytes,
+                     "kernel": "coder_step_kernel<float,false>", "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nb = np.asarray([len(b) for b in payload_bits], dtype=np.int64)
+        stride = int((nb.max() + 7) // 8)
+        pl = np.zeros((B, stride), np.uint8)
+        for i, b in enumerate(payload_bits[:64]):
+            pk = np.packbits(np.asarray(b, np.uint8), bitorder="little")
+            pl[i, : pk.size] = pk
+        Bs = 16
+        pool_h = [p[:Bs].float().cpu().numpy() for p in pool[:2]]
+        out["cpu_baseline"] = cpu_baseline(pool_h, pl, nb, args, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

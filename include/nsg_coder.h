@@ -1,0 +1,122 @@
+/*
+ * nsg_coder.h -- C ABI of the MI355X (gfx950) batched arithmetic-coding step library `libnsgcoder.so`.
+ *
+ * One call runs ONE coder step for B independent message streams on a [B, ld] logit matrix that is
+ * already resident in HBM.  The work is stream-ordered on the caller's hipStream_t (passed as void*);
+ * no call allocates, synchronises or copies except ns_create / ns_destroy / ns_read_counters.
+ *
+ * What each entry point replaces in the reference (nobkagit/NeuralSteganography):
+ *
+ *   ns_encode_step  -- one iteration of the `while i < len(message)` loop body of
+ *                      code_base/arithmetic.py:124-203 (ban, sort, float64 softmax, cutoff k
+ *                      (_select_cutoff_k :51-75), integer CDF :143-165, bit consume :167-190, token
+ *                      append :202), batched over B streams.  The Python loop that calls it replaces
+ *                      encode_arithmetic (code_base/arithmetic.py:78-217) and, behind the provider
+ *                      protocol, src/neuralstego/lm/arithmetic.py:162-191 (ArithmeticLM.encode_arithmetic).
+ *   ns_decode_step  -- one iteration of code_base/arithmetic.py:255-371 (same CDF, rank lookup :298,
+ *                      bit emit :354-360), batched; replaces decode_arithmetic (:220-373) and
+ *                      src/neuralstego/lm/arithmetic.py:193-226.  A received token outside the kept top-k
+ *                      is reported per stream (NS_ST_ERR_DIVERGE) instead of running the BPE-repair
+ *                      heuristics of :300-342 (those need the tokenizer; the host applies them).
+ *   ns_init_state   -- `cur_interval = [0, 2**precision]`, `i = 0` (code_base/arithmetic.py:96-98,112).
+ *
+ * Bit conventions: payload bytes are read LSB-first (bit j = byte[j>>3] >> (j&7)), the order in which
+ * src/neuralstego/api.py:153-157 turns bytes into the bit list the coder consumes; within a step the
+ * next `precision` bits form an MSB-first integer (code_base/arithmetic.py:168-171).  Decoded bits are
+ * written back in the same LSB-first packing.
+ *
+ * Errors: return NS_OK (0) or a negative NS_ERR_*; ns_last_error() gives a message.  Per-stream coder
+ * failures (the reference's ArithmeticRangeError / DecodeDivergenceError, src/neuralstego/codec/errors.py:10-15)
+ * are flags in ns_stream_state.flags; the Python host raises them.
+ */
+#ifndef NSG_CODER_H
+#define NSG_CODER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NS_OK 0
+#define NS_ERR_CONFIG -1      /* bad argument: maps to ConfigurationError / ValueError          */
+#define NS_ERR_UNSUPPORTED -2 /* valid for the reference, not (yet) for this kernel (topk too large) */
+#define NS_ERR_HIP -3         /* HIP runtime error (launch failure)                             */
+
+#define NS_DTYPE_F32 0
+#define NS_DTYPE_F16 1
+
+/* per-stream flags */
+#define NS_ST_DONE 1u         /* encode: all payload bits consumed; no further tokens are produced */
+#define NS_ST_ERR_RANGE 2u    /* no CDF bucket above the payload index (ArithmeticRangeError)      */
+#define NS_ST_ERR_DIVERGE 4u  /* decode: received token not in the kept top-k (DecodeDivergenceError) */
+#define NS_ST_EXACT_SUM 8u    /* the last step needed the exact float64 row sum (slow path taken)   */
+
+/* step flags */
+#define NS_STEP_FORCE_EXACT_SUM 1u /* always take the exact-sum path (parity testing) */
+
+#define NS_MAX_BANNED 8
+
+typedef struct ns_stream_state {
+    uint64_t lo;      /* interval bottom (inclusive)                                    */
+    uint64_t hi;      /* interval top (exclusive)                                       */
+    int64_t bit_pos;  /* encode: payload bits fixed so far (`i`); decode: bits emitted  */
+    int32_t ntokens;  /* tokens produced (encode) / consumed (decode)                   */
+    uint32_t flags;   /* NS_ST_*                                                        */
+} ns_stream_state;
+
+typedef struct ns_step_trace { /* optional per-stream record of the last step (tests, debugging) */
+    int32_t k;      /* kept candidates after the 1/R cutoff and topk                   */
+    int32_t kprime; /* after the overfill trim                                         */
+    int32_t sel;    /* selected rank                                                   */
+    int32_t n;      /* bits fixed (encode) / emitted before the last-token rule (decode) */
+    int32_t token;  /* token id emitted / consumed                                     */
+    int32_t exact;  /* 1 if the exact float64 row sum was computed                     */
+    double S;       /* row sum used for the cutoff (fast estimate or exact)            */
+} ns_step_trace;
+
+typedef struct ns_ctx ns_ctx;
+
+/* Create a context on `device` for logits rows of `vocab` entries of `logits_dtype` (NS_DTYPE_*),
+ * at most `max_batch` streams per call, interval precision `precision` (1..60 bits) and top-k up to
+ * `max_k` (must be <= ns_max_topk(logits_dtype)).  Returns NULL on failure (see ns_last_error(NULL)). */
+ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision, int logits_dtype);
+void ns_destroy(ns_ctx* ctx);
+const char* ns_last_error(const ns_ctx* ctx);
+const char* ns_version(void);
+
+/* Largest topk the single-pass kernel supports for a logits dtype. */
+int ns_max_topk(int logits_dtype);
+
+/* Reset B stream states to [0, 2^precision), bit_pos 0. */
+int ns_init_state(ns_ctx* ctx, ns_stream_state* d_state, int B, void* hip_stream);
+
+/* One encode step for streams [0,B).  d_logits: [B, ld] row-major, 16-byte aligned, ld a multiple of
+ * 16/sizeof(dtype) and >= vocab.  d_payload: [B, payload_stride] bytes, d_payload_nbits: [B] int64.
+ * d_out_token: [B] (written for every stream that produced a token this step).  d_token_hist: optional
+ * [B, hist_stride] history, token t of stream b at b*hist_stride+t.  banned: HOST array of nbanned ids
+ * (<= NS_MAX_BANNED), the reference bans {vocab-1, 628}.  d_trace: optional [B].  temp > 0. */
+int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const uint8_t* d_payload,
+                   int64_t payload_stride, const int64_t* d_payload_nbits, ns_stream_state* d_state,
+                   int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride, double temp, int topk,
+                   const int32_t* banned, int nbanned, ns_step_trace* d_trace, uint32_t step_flags,
+                   void* hip_stream);
+
+/* One decode step.  d_in_token: [B] received token of this step; d_is_last: [B] nonzero when it is the
+ * stream's last token (then all `precision` bits of the new bottom are emitted, arithmetic.py:356-357).
+ * d_out_bits: [B, out_stride] bytes, bits appended LSB-first at ns_stream_state.bit_pos.
+ * d_active: optional [B] mask; streams with 0 are skipped (ragged token counts). */
+int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const int32_t* d_in_token,
+                   const uint8_t* d_is_last, const uint8_t* d_active, ns_stream_state* d_state,
+                   uint8_t* d_out_bits, int64_t out_stride, double temp, int topk, const int32_t* banned,
+                   int nbanned, ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
+
+/* Diagnostics: counters[0] = stream-steps run, counters[1] = stream-steps that took the exact-sum path,
+ * counters[2] = candidate-buffer compactions.  Synchronises the device. */
+int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters3);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NSG_CODER_H */

@@ -1,0 +1,88 @@
+"""ctypes binding of ``libnsgcoder.so`` (C ABI declared in ``include/nsg_coder.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``hipcc --offload-arch=gfx950``).  There is
+no CPU fallback: if the shared object is missing or cannot be loaded, :func:`lib` raises, and every
+coder entry point fails loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "_build" / "libnsgcoder.so"
+
+NS_OK, NS_ERR_CONFIG, NS_ERR_UNSUPPORTED, NS_ERR_HIP = 0, -1, -2, -3
+NS_DTYPE_F32, NS_DTYPE_F16 = 0, 1
+NS_ST_DONE, NS_ST_ERR_RANGE, NS_ST_ERR_DIVERGE, NS_ST_EXACT_SUM = 1, 2, 4, 8
+NS_STEP_FORCE_EXACT_SUM = 1
+NS_MAX_BANNED = 8
+
+EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
+           "ns_encode_step", "ns_decode_step", "ns_read_counters")
+
+
+class NsStreamState(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64), ("bit_pos", ctypes.c_int64),
+                ("ntokens", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class NsStepTrace(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("kprime", ctypes.c_int32), ("sel", ctypes.c_int32),
+                ("n", ctypes.c_int32), ("token", ctypes.c_int32), ("exact", ctypes.c_int32),
+                ("S", ctypes.c_double)]
+
+
+assert ctypes.sizeof(NsStreamState) == 32 and ctypes.sizeof(NsStepTrace) == 32
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP coder library is missing or unusable (never silently replaced by a CPU path)."""
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryError(
+            f"{LIB_PATH} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    try:
+        L = ctypes.CDLL(str(LIB_PATH))
+    except OSError as exc:  # pragma: no cover - environment specific
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {exc}") from exc
+    vp, i32p, u8p, i64p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p, ctypes.c_void_p
+    L.ns_create.restype = vp
+    L.ns_create.argtypes = [ctypes.c_int] * 6
+    L.ns_destroy.restype = None
+    L.ns_destroy.argtypes = [vp]
+    L.ns_last_error.restype = ctypes.c_char_p
+    L.ns_last_error.argtypes = [vp]
+    L.ns_version.restype = ctypes.c_char_p
+    L.ns_version.argtypes = []
+    L.ns_max_topk.restype = ctypes.c_int
+    L.ns_max_topk.argtypes = [ctypes.c_int]
+    L.ns_init_state.restype = ctypes.c_int
+    L.ns_init_state.argtypes = [vp, vp, ctypes.c_int, vp]
+    L.ns_encode_step.restype = ctypes.c_int
+    L.ns_encode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, u8p, ctypes.c_int64, i64p, vp, vp, vp,
+                                 ctypes.c_int64, ctypes.c_double, ctypes.c_int, i32p, ctypes.c_int, vp,
+                                 ctypes.c_uint32, vp]
+    L.ns_decode_step.restype = ctypes.c_int
+    L.ns_decode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int64,
+                                 ctypes.c_double, ctypes.c_int, i32p, ctypes.c_int, vp, ctypes.c_uint32, vp]
+    L.ns_read_counters.restype = ctypes.c_int
+    L.ns_read_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    _lib = L
+    return L
+
+
+def version() -> str:
+    return lib().ns_version().decode()
+
+
+def max_topk(dtype_code: int) -> int:
+    return int(lib().ns_max_topk(int(dtype_code)))

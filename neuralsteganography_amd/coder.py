@@ -1,0 +1,317 @@
+"""Batched arithmetic-coding sessions on the HIP coder (``libnsgcoder.so``).
+
+A session owns the device buffers of B independent streams and launches one coder step per call on the
+current torch stream.  It is the batched replacement of the per-stream loops in
+``code_base/arithmetic.py:112-210`` (encode) and ``:254-371`` (decode): the caller supplies the ``[B, ld]``
+logits of each step (a GPT-2 forward, or synthetic rows) and the kernel does sort/softmax/CDF/interval
+work for all B streams at once.
+
+All device state lives in torch tensors (PyTorch is plumbing here); the arithmetic runs only in the HIP
+kernel.  There is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .codec.errors import ArithmeticRangeError, DecodeDivergenceError
+from .exceptions import ConfigurationError
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream_handle():
+    torch = _torch()
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def row_stride(vocab: int, dtype: str) -> int:
+    """Padded logits row stride the kernel wants: a multiple of 64 elements (16-byte vectors, 256-B rows)."""
+    _ = dtype
+    return ((vocab + 63) // 64) * 64
+
+
+@dataclass(frozen=True)
+class CoderParams:
+    """Coder parameters of ``encode_arithmetic``/``decode_arithmetic`` (``code_base/arithmetic.py:78-88``)."""
+
+    vocab: int
+    precision: int = 26
+    temp: float = 0.9
+    topk: int = 300
+    dtype: str = "f32"  # logits dtype: "f32" or "f16"
+    banned: Optional[Sequence[int]] = None  # default: (vocab-1, 628) as arithmetic.py:124-125
+
+    def banned_ids(self) -> List[int]:
+        if self.banned is not None:
+            return [int(b) for b in self.banned]
+        return [self.vocab - 1, 628]
+
+    @property
+    def dtype_code(self) -> int:
+        if self.dtype == "f32":
+            return _lib.NS_DTYPE_F32
+        if self.dtype == "f16":
+            return _lib.NS_DTYPE_F16
+        raise ConfigurationError(f"unsupported logits dtype {self.dtype!r}")
+
+    @property
+    def torch_dtype(self):
+        torch = _torch()
+        return torch.float16 if self.dtype == "f16" else torch.float32
+
+    def validate(self) -> None:
+        if self.vocab < 2:
+            raise ConfigurationError("vocab must be >= 2")
+        if not 1 <= self.precision <= 60:
+            raise ConfigurationError("precision must be within [1, 60]")
+        if not self.temp > 0:
+            raise ConfigurationError("temperature must be positive")
+        if self.topk < 1:
+            raise ConfigurationError("topk must be positive")
+        if len(self.banned_ids()) > _lib.NS_MAX_BANNED:
+            raise ConfigurationError(f"at most {_lib.NS_MAX_BANNED} banned ids")
+
+
+class CoderContext:
+    """Owns an ``ns_ctx`` (device, vocab, precision, dtype, max batch)."""
+
+    def __init__(self, params: CoderParams, max_batch: int, device: Optional[int] = None):
+        params.validate()
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise _lib.NativeLibraryError("the HIP coder needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.params = params
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.max_batch = int(max_batch)
+        L = _lib.lib()
+        kmax = L.ns_max_topk(params.dtype_code)
+        vocab_valid = params.vocab - len({b for b in params.banned_ids() if 0 <= b < params.vocab})
+        self.K = min(params.topk, vocab_valid)
+        if self.K > kmax:
+            raise ConfigurationError(
+                f"topk={params.topk} exceeds the single-pass HIP kernel limit {kmax} for {params.dtype} logits")
+        handle = L.ns_create(self.device, self.max_batch, params.vocab, max(1, self.K), params.precision,
+                             params.dtype_code)
+        if not handle:
+            raise _lib.NativeLibraryError(f"ns_create failed: {L.ns_last_error(None).decode()}")
+        self._h = ctypes.c_void_p(handle)
+        self._banned = (ctypes.c_int32 * max(1, len(params.banned_ids())))(*params.banned_ids())
+        self._nbanned = len(params.banned_ids())
+
+    def check(self, rc: int, what: str) -> None:
+        if rc != _lib.NS_OK:
+            msg = _lib.lib().ns_last_error(self._h).decode()
+            if rc == _lib.NS_ERR_CONFIG:
+                raise ConfigurationError(f"{what}: {msg}")
+            raise _lib.NativeLibraryError(f"{what}: rc={rc}: {msg}")
+
+    def counters(self) -> List[int]:
+        out = (ctypes.c_uint64 * 3)()
+        self.check(_lib.lib().ns_read_counters(self._h, out), "ns_read_counters")
+        return [int(v) for v in out]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().ns_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _state_tensor(B: int, device):
+    torch = _torch()
+    return torch.zeros((B, 4), dtype=torch.int64, device=device)
+
+
+def _state_fields(state) -> dict:
+    """Host view of [B,4] int64 state rows: lo, hi, bit_pos, ntokens, flags."""
+    s = state.cpu().numpy()
+    w32 = s.view(np.int32).reshape(s.shape[0], 8)
+    return {"lo": s[:, 0].view(np.uint64), "hi": s[:, 1].view(np.uint64), "bit_pos": s[:, 2],
+            "ntokens": w32[:, 6], "flags": w32[:, 7].view(np.uint32)}
+
+
+class EncodeSession:
+    """B streams being encoded; call :meth:`step` once per generated token with that step's logits."""
+
+    def __init__(self, ctx: CoderContext, payload_bits: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        torch = _torch()
+        self.ctx = ctx
+        self.B = len(payload_bits)
+        if self.B < 1 or self.B > ctx.max_batch:
+            raise ConfigurationError(f"batch {self.B} outside [1, {ctx.max_batch}]")
+        dev = torch.device("cuda", ctx.device)
+        self.nbits_host = np.asarray([len(b) for b in payload_bits], dtype=np.int64)
+        stride = max(1, int((self.nbits_host.max() + 7) // 8))
+        pl = np.zeros((self.B, stride), dtype=np.uint8)
+        for i, bits in enumerate(payload_bits):
+            if len(bits):
+                packed = np.packbits(np.asarray(bits, dtype=np.uint8), bitorder="little")
+                pl[i, : packed.size] = packed
+        self.payload = torch.from_numpy(pl).to(dev)
+        self.nbits = torch.from_numpy(self.nbits_host).to(dev)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        self.out_token = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        cap = max_tokens if max_tokens is not None else int(2 * self.nbits_host.max() + 64)
+        self.hist = torch.full((self.B, cap), -1, dtype=torch.int32, device=dev)
+        self.trace = None
+        self.steps = 0
+
+    def enable_trace(self):
+        torch = _torch()
+        self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
+        return self.trace
+
+    def step(self, logits, *, force_exact: bool = False):
+        """One coder step on ``logits`` ([B, ld] contiguous rows, ld = :func:`row_stride`)."""
+        p = self.ctx.params
+        self._check_logits(logits)
+        flags = _lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0
+        rc = _lib.lib().ns_encode_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
+            _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), self.hist.shape[1],
+            float(p.temp), int(p.topk), self.ctx._banned, self.ctx._nbanned, _ptr(self.trace), flags,
+            _stream_handle())
+        self.ctx.check(rc, "ns_encode_step")
+        self.steps += 1
+        return self.out_token
+
+    def _check_logits(self, logits) -> None:
+        p = self.ctx.params
+        if logits.dtype != p.torch_dtype or logits.dim() != 2 or logits.shape[0] != self.B:
+            raise ConfigurationError(f"logits must be [{self.B}, ld] {p.dtype}")
+        if logits.stride(1) != 1 or logits.shape[1] < p.vocab or not logits.is_cuda:
+            raise ConfigurationError("logits must be contiguous rows on the GPU with ld >= vocab")
+
+    def all_done(self) -> bool:
+        return bool(np.all(_state_fields(self.state)["flags"] & _lib.NS_ST_DONE))
+
+    def fields(self) -> dict:
+        return _state_fields(self.state)
+
+    def raise_errors(self) -> None:
+        f = self.fields()["flags"]
+        bad = np.nonzero(f & _lib.NS_ST_ERR_RANGE)[0]
+        if bad.size:
+            raise ArithmeticRangeError(f"streams {bad.tolist()[:8]} found no CDF bucket for the payload index")
+
+    def tokens(self) -> List[List[int]]:
+        self.raise_errors()
+        f = self.fields()
+        if int(f["ntokens"].max(initial=0)) > self.hist.shape[1]:
+            raise ConfigurationError("token history overflow: raise max_tokens")
+        h = self.hist.cpu().numpy()
+        return [h[i, : int(f["ntokens"][i])].astype(np.int64).tolist() for i in range(self.B)]
+
+    def trace_rows(self) -> np.ndarray:
+        """Last-step trace as a structured host array (k, kprime, sel, n, token, exact, S)."""
+        raw = self.trace.cpu().numpy()
+        w = raw.view(np.int32).reshape(self.B, 8)
+        return np.rec.fromarrays([w[:, 0], w[:, 1], w[:, 2], w[:, 3], w[:, 4], w[:, 5], raw[:, 3].view(np.float64)],
+                                 names="k,kprime,sel,n,token,exact,S")
+
+
+class DecodeSession:
+    """B received token streams (ragged) being decoded back to bits."""
+
+    def __init__(self, ctx: CoderContext, token_lists: Sequence[Sequence[int]]):
+        torch = _torch()
+        self.ctx = ctx
+        self.B = len(token_lists)
+        if self.B < 1 or self.B > ctx.max_batch:
+            raise ConfigurationError(f"batch {self.B} outside [1, {ctx.max_batch}]")
+        dev = torch.device("cuda", ctx.device)
+        self.lens = np.asarray([len(t) for t in token_lists], dtype=np.int64)
+        self.T = int(self.lens.max(initial=0))
+        tok = np.zeros((max(self.T, 1), self.B), dtype=np.int32)
+        last = np.zeros((max(self.T, 1), self.B), dtype=np.uint8)
+        act = np.zeros((max(self.T, 1), self.B), dtype=np.uint8)
+        for i, tl in enumerate(token_lists):
+            n = len(tl)
+            if n:
+                tok[:n, i] = np.asarray(tl, dtype=np.int32)
+                last[n - 1, i] = 1
+                act[:n, i] = 1
+        self.tok = torch.from_numpy(tok).to(dev)
+        self.last = torch.from_numpy(last).to(dev)
+        self.act = torch.from_numpy(act).to(dev)
+        P = ctx.params.precision
+        self.out_stride = int((self.T * P + P + 7) // 8 + 8)
+        self.out_bits = torch.zeros((self.B, self.out_stride), dtype=torch.uint8, device=dev)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        self.trace = None
+        self.t = 0
+
+    def enable_trace(self):
+        torch = _torch()
+        self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
+        return self.trace
+
+    def step(self, logits, *, force_exact: bool = False) -> None:
+        p = self.ctx.params
+        if self.t >= self.T:
+            raise ConfigurationError("all tokens already decoded")
+        t = self.t
+        flags = _lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0
+        rc = _lib.lib().ns_decode_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok[t]), _ptr(self.last[t]),
+            _ptr(self.act[t]), _ptr(self.state), _ptr(self.out_bits), self.out_stride, float(p.temp),
+            int(p.topk), self.ctx._banned, self.ctx._nbanned, _ptr(self.trace), flags, _stream_handle())
+        self.ctx.check(rc, "ns_decode_step")
+        self.t += 1
+
+    def bits(self) -> List[List[int]]:
+        f = _state_fields(self.state)
+        bad = np.nonzero(f["flags"] & _lib.NS_ST_ERR_DIVERGE)[0]
+        if bad.size:
+            raise DecodeDivergenceError(f"streams {bad.tolist()[:8]}: received token outside the kept top-k")
+        ob = self.out_bits.cpu().numpy()
+        out = []
+        for i in range(self.B):
+            nb = int(f["bit_pos"][i])
+            out.append(np.unpackbits(ob[i], bitorder="little")[:nb].astype(np.int64).tolist())
+        return out
+
+
+def encode_batch(ctx: CoderContext, payload_bits: Sequence[Sequence[int]], logits_fn, *, max_steps: int = 1 << 20,
+                 check_every: int = 32, force_exact: bool = False) -> List[List[int]]:
+    """Run encode steps until every stream has consumed its payload; ``logits_fn(step, last_tokens)``
+    returns the ``[B, ld]`` logits of that step."""
+    sess = EncodeSession(ctx, payload_bits)
+    last = sess.out_token
+    for t in range(max_steps):
+        if t % check_every == 0 and sess.all_done():
+            break
+        last = sess.step(logits_fn(t, last), force_exact=force_exact)
+    else:
+        raise ConfigurationError("encode did not finish within max_steps")
+    return sess.tokens()
+
+
+def decode_batch(ctx: CoderContext, token_lists: Sequence[Sequence[int]], logits_fn, *,
+                 force_exact: bool = False) -> List[List[int]]:
+    sess = DecodeSession(ctx, token_lists)
+    for t in range(sess.T):
+        sess.step(logits_fn(t, sess.tok[t]), force_exact=force_exact)
+    return sess.bits()

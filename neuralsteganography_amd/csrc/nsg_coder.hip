@@ -1,0 +1,848 @@
+// nsg_coder.hip -- batched arithmetic-coding step for MI355X (gfx950 / CDNA4), C ABI in include/nsg_coder.h.
+//
+// One wavefront (64 lanes) owns one message stream per step.  The [B, ld] logit matrix is streamed from
+// HBM once, 16 bytes per lane per load (global_load_dwordx4), several tiles in flight per wave.  While
+// streaming, every wave keeps
+//   * a float64 estimate of the softmax denominator (hardware v_exp_f32 on a fixed per-row reference,
+//     fp32 partials flushed into a float64 accumulator per tile) with a rigorous error bound, and
+//   * a candidate buffer in LDS of (value desc, id asc) keys above a running threshold; when it fills it
+//     is compacted to the exact top-K by a ballot/popcount bisection (no sort).
+// After the row, the top-K candidates are ranked (one LDS broadcast read per key), and the whole CDF
+// step (canonical float64 exp, 1/R cutoff, rint, int64 prefix sum, overfill trim, interval update,
+// bit consume / emit) runs across the wave's lanes with DPP/bpermute shuffles.
+//
+// Exactness contract: results are bit-identical to oracle/nsg_oracle.c (the canonical restatement of
+// code_base/arithmetic.py).  Everything that feeds the emitted integers is computed in the canonical
+// float64 order; the fast denominator is used only where its error bound proves the 1/R cutoff decision
+// (arithmetic.py:140-142) cannot differ from the exact one -- otherwise the wave re-reads its row and
+// computes the exact canonical sum (NS_ST_EXACT_SUM).
+//
+// Build (see __graft_entry__.build): hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/nsg_coder.h"
+
+#pragma clang fp contract(off)
+
+namespace nsg {
+
+constexpr int WAVE = 64;
+constexpr int WPB = 4;        // waves (streams) per workgroup
+constexpr int CAND = 1024;    // candidate keys per wave (8 KiB LDS)
+constexpr int PREFETCH = 4;   // tiles in flight per wave
+
+// ------------------------------------------------------------------------------------------------
+// canonical float64 exp -- identical operation sequence to or_exp_canon (oracle/nsg_oracle.c)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double exp_canon(double d) {
+    if (!(d >= -700.0)) return 0.0;
+    const double n = __builtin_rint(d * 1.44269504088896338700e+00);
+    double r = __builtin_fma(-n, 6.93147180369123816490e-01, d);
+    r = __builtin_fma(-n, 1.90821492927058770002e-10, r);
+    double p = 1.60590438368216145994e-10;
+    p = __builtin_fma(p, r, 2.08767569878680989792e-09);
+    p = __builtin_fma(p, r, 2.50521083854417187751e-08);
+    p = __builtin_fma(p, r, 2.75573192239858906526e-07);
+    p = __builtin_fma(p, r, 2.75573192239858906526e-06);
+    p = __builtin_fma(p, r, 2.48015873015873015873e-05);
+    p = __builtin_fma(p, r, 1.98412698412698412698e-04);
+    p = __builtin_fma(p, r, 1.38888888888888888889e-03);
+    p = __builtin_fma(p, r, 8.33333333333333333333e-03);
+    p = __builtin_fma(p, r, 4.16666666666666666667e-02);
+    p = __builtin_fma(p, r, 1.66666666666666666667e-01);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
+
+// ------------------------------------------------------------------------------------------------
+// keys: (value desc, id asc) as one descending uint64
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord32(float x) {
+    x = x + 0.0f;  // -0 -> +0
+    const uint32_t u = __float_as_uint(x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord32(uint32_t o) {
+    const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    return __uint_as_float(u);
+}
+__device__ __forceinline__ uint64_t make_key(float x, uint32_t j) {
+    return ((uint64_t)ord32(x) << 32) | (uint64_t)(0xFFFFFFFFu - j);
+}
+__device__ __forceinline__ uint32_t key_id(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ float key_val(uint64_t k) { return unord32((uint32_t)(k >> 32)); }
+
+// ------------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ void lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ double wave_sum_butterfly(double v) {
+    // canonical xor butterfly 32,16,8,4,2,1 (commutative per pair => every lane ends identical)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const int64_t y = __shfl_up(v, off);
+        if (lane >= off) v += y;
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// logit loads
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct Elem;
+template <>
+struct Elem<float> {
+    static constexpr int W = 4;
+    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[4]) {
+        x[0] = __uint_as_float(v.x);
+        x[1] = __uint_as_float(v.y);
+        x[2] = __uint_as_float(v.z);
+        x[3] = __uint_as_float(v.w);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int j) { return ((const float*)row)[j]; }
+};
+template <>
+struct Elem<_Float16> {
+    static constexpr int W = 8;
+    __device__ static __forceinline__ float h2f(uint32_t bits16) {
+        const uint16_t b = (uint16_t)bits16;
+        _Float16 h;
+        __builtin_memcpy(&h, &b, 2);
+        return (float)h;
+    }
+    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[8]) {
+        x[0] = h2f(v.x & 0xFFFFu);
+        x[1] = h2f(v.x >> 16);
+        x[2] = h2f(v.y & 0xFFFFu);
+        x[3] = h2f(v.y >> 16);
+        x[4] = h2f(v.z & 0xFFFFu);
+        x[5] = h2f(v.z >> 16);
+        x[6] = h2f(v.w & 0xFFFFu);
+        x[7] = h2f(v.w >> 16);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int j) {
+        return h2f(((const uint16_t*)row)[j]);
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// step parameters (kernel argument, by value)
+// ------------------------------------------------------------------------------------------------
+struct StepParams {
+    const void* logits;
+    int64_t ld;
+    int B, V, P, topk, K;  // K = min(topk, #valid ids)
+    double inv_temp;
+    float c32;  // (float)(inv_temp * log2(e))
+    int nbanned;
+    int banned[NS_MAX_BANNED];  // sorted ascending, unique, in [0, V)
+    uint32_t flags;
+    // encode
+    const uint8_t* payload;
+    int64_t payload_stride;
+    const int64_t* nbits;
+    int32_t* out_token;
+    int32_t* hist;
+    int64_t hist_stride;
+    // decode
+    const int32_t* in_token;
+    const uint8_t* is_last;
+    const uint8_t* active;
+    uint8_t* out_bits;
+    int64_t out_stride;
+    // common
+    ns_stream_state* state;
+    ns_step_trace* trace;
+    unsigned long long* counters;
+};
+
+__device__ __forceinline__ bool is_banned(const StepParams& p, int j) {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NS_MAX_BANNED; ++i) b |= (i < p.nbanned) && (p.banned[i] == j);
+    return b;
+}
+
+// exact canonical row sum (oracle or_row_sum): id j -> lane (j>>2)&63, per-lane increasing, butterfly
+template <typename T>
+__device__ __noinline__ double exact_row_sum(const StepParams& p, const void* row, double m, int lane) {
+    double acc = 0.0;
+    const int ngroups = (p.V + 3) >> 2;
+    for (int g = lane; g < ngroups; g += WAVE) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 4 * g + q;
+            if (j < p.V && !is_banned(p, j)) {
+                const float x = Elem<T>::load1(row, j) + 0.0f;
+                acc += exp_canon(((double)x - m) * p.inv_temp);
+            }
+        }
+    }
+    return wave_sum_butterfly(acc);
+}
+
+// Keep exactly the top-K keys of keys[0..cnt) (cnt >= K).  Bisection on the value word, then on the id
+// word among ties; counts by ballot+popcount.  Returns the K-th key.
+__device__ __noinline__ uint64_t compact_topk(uint64_t* keys, int cnt, int K, int lane) {
+    constexpr int NSL = CAND / WAVE;
+    uint64_t kr[NSL];
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+        const int i = s * WAVE + lane;
+        kr[s] = (i < cnt) ? keys[i] : 0ull;  // real keys are > 0
+    }
+    const int nsl = (cnt + WAVE - 1) / WAVE;
+    uint32_t v = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = v | (1u << bit);
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < NSL; ++s)
+            if (s < nsl) c += popc64(ballot((uint32_t)(kr[s] >> 32) >= cand));
+        if (c >= K) v = cand;
+    }
+    int c_gt = 0, c_eq = 0;
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+        if (s < nsl) {
+            const uint32_t h = (uint32_t)(kr[s] >> 32);
+            c_gt += popc64(ballot(h > v));
+            c_eq += popc64(ballot(h == v));
+        }
+    }
+    const int need = K - c_gt;
+    uint32_t wlo = 0;
+    if (c_eq > need) {
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cand = wlo | (1u << bit);
+            int c = 0;
+#pragma unroll
+            for (int s = 0; s < NSL; ++s)
+                if (s < nsl) c += popc64(ballot((uint32_t)(kr[s] >> 32) == v && (uint32_t)kr[s] >= cand));
+            if (c >= need) wlo = cand;
+        }
+    }
+    const uint64_t kappa = ((uint64_t)v << 32) | wlo;
+    lds_fence();
+    int base = 0;
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+        if (s < nsl) {
+            const bool keep = kr[s] >= kappa && kr[s] != 0ull;
+            const uint64_t m = ballot(keep);
+            if (keep) keys[base + lanes_below(m)] = kr[s];
+            base += popc64(m);
+        }
+    }
+    lds_fence();
+    return kappa;
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
+    constexpr int W = Elem<T>::W;
+    constexpr int TS = WAVE * W;               // elements per tile
+    constexpr int NSK = (CAND - TS) / WAVE;    // sorted-rank slots per lane (K <= CAND - TS)
+    __shared__ uint64_t s_keys[WPB][CAND];
+
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    const int b = blockIdx.x * WPB + wv;
+    if (b >= p.B) return;
+    uint64_t* keys = s_keys[wv];
+
+    ns_stream_state st = p.state[b];
+    if (st.flags & NS_ST_DONE) return;
+    int64_t nbits = 0;
+    if (!DECODE) {
+        nbits = p.nbits[b];
+        if (st.bit_pos >= nbits) {
+            if (lane == 0) p.state[b].flags = st.flags | NS_ST_DONE;
+            return;
+        }
+    } else {
+        if (p.active && !p.active[b]) return;
+    }
+
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const uint4* rowv = (const uint4*)rowc;
+    const int V = p.V;
+    const int nvec = (V + W - 1) / W;
+    const int ntiles = (nvec + WAVE - 1) / WAVE;
+
+    // ---------------- streaming pass ----------------
+    float tau = -__builtin_inff();
+    int cnt = 0;
+    int ncompact = 0;
+    float r = 0.0f;
+    double acc64 = 0.0;
+    int bi = 0;
+    int next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+    const float c32 = p.c32;
+
+    uint4 buf[PREFETCH];
+#pragma unroll
+    for (int d = 0; d < PREFETCH; ++d) {
+        const int v = d * WAVE + lane;
+        buf[d] = (d < ntiles && v < nvec) ? rowv[v] : make_uint4(0u, 0u, 0u, 0u);
+    }
+
+    for (int t0 = 0; t0 < ntiles; t0 += PREFETCH) {
+        uint4 nxt[PREFETCH];
+#pragma unroll
+        for (int d = 0; d < PREFETCH; ++d) {
+            const int v = (t0 + PREFETCH + d) * WAVE + lane;
+            nxt[d] = (t0 + PREFETCH + d < ntiles && v < nvec) ? rowv[v] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int d = 0; d < PREFETCH; ++d) {
+            const int tile = t0 + d;
+            if (tile < ntiles) {
+                const int v = tile * WAVE + lane;
+                const int j0 = v * W;
+                float x[W];
+                Elem<T>::unpack(buf[d], x);
+#pragma unroll
+                for (int q = 0; q < W; ++q)
+                    if (j0 + q >= V) x[q] = -__builtin_inff();
+                const int tile_end = (tile + 1) * TS;
+                while (next_ban < tile_end) {  // wave-uniform, rare
+#pragma unroll
+                    for (int q = 0; q < W; ++q)
+                        if (j0 + q == next_ban) x[q] = -__builtin_inff();
+                    ++bi;
+                    next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+                }
+                if (tile == 0) {
+                    float mx = x[0];
+#pragma unroll
+                    for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+                    r = wave_max(mx);
+                    if (r == -__builtin_inff()) r = 0.0f;
+                }
+                // softmax denominator estimate (fast path)
+                float a = 0.0f;
+#pragma unroll
+                for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((x[q] - r) * c32);
+                acc64 += (double)a;
+                // candidates
+                float mx = x[0];
+#pragma unroll
+                for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+                if (ballot(mx > tau)) {
+                    uint64_t msk[W];
+                    int npt = 0;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        msk[q] = ballot(x[q] > tau);
+                        npt += popc64(msk[q]);
+                    }
+                    if (cnt + npt > CAND) {
+                        const uint64_t kappa = compact_topk(keys, cnt, p.K, lane);
+                        ++ncompact;
+                        cnt = p.K;
+                        tau = unord32((uint32_t)(kappa >> 32));
+                        npt = 0;
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            msk[q] = ballot(x[q] > tau);
+                            npt += popc64(msk[q]);
+                        }
+                    }
+                    int base = cnt;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        if (x[q] > tau) keys[base + lanes_below(msk[q])] = make_key(x[q], (uint32_t)(j0 + q));
+                        base += popc64(msk[q]);
+                    }
+                    cnt = base;
+                }
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < PREFETCH; ++d) buf[d] = nxt[d];
+    }
+    lds_fence();
+
+    // ---------------- exact top-K, ranked ----------------
+    const int K = p.K;
+    if (cnt > K) {
+        compact_topk(keys, cnt, K, lane);
+        ++ncompact;
+    }
+    uint64_t sk[NSK];
+    int rk[NSK];
+    const int nsk = (K + WAVE - 1) / WAVE;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        sk[s] = (s < nsk && i < K) ? keys[i] : 0ull;
+        rk[s] = 0;
+    }
+    for (int t = 0; t < K; ++t) {
+        const uint64_t o = keys[t];  // LDS broadcast
+#pragma unroll
+        for (int s = 0; s < NSK; ++s)
+            if (s < nsk) rk[s] += (o > sk[s]) ? 1 : 0;
+    }
+    lds_fence();
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        if (s < nsk && i < K) keys[rk[s]] = sk[s];
+    }
+    lds_fence();
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        sk[s] = (s < nsk && i < K) ? keys[i] : 0ull;
+    }
+
+    // ---------------- CDF step (canonical float64) ----------------
+    const double m = (double)key_val(keys[0]);
+    double e[NSK];
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        e[s] = (s < nsk && i < K) ? exp_canon(((double)key_val(sk[s]) - m) * p.inv_temp) : 0.0;
+    }
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R;
+    const double thr = 1.0 / Rd;
+
+    // fast denominator with a rigorous interval
+    const double S_r = wave_sum_butterfly(acc64);
+    const double t_m = (m - (double)r) * (double)c32;
+    bool exact = (p.flags & NS_STEP_FORCE_EXACT_SUM) != 0u;
+    exact = exact || !(S_r > 0.0 && S_r < 1.0e300) || !(t_m <= 100.0 && t_m >= -60.0);
+    double S_used;
+    int k0 = K;
+    if (!exact) {
+        const double f = exp_canon(((double)r - m) * p.inv_temp);
+        const double Sf = S_r * f;
+        const double u24 = 5.9604644775390625e-08;  // 2^-24
+        const double eb = 9.5367431640625e-07         // v_exp_f32 error (2^-20, generous)
+                          + 3.0 * u24 * 0.6931471805599453 * (60.0 + fabs(t_m))  // argument rounding
+                          + (double)(W + 1) * u24                                   // fp32 partials
+                          + 1.0e-13;
+        const double B2 = 2.0 * eb + 1.0e-12;
+        const double S_lo = Sf * (1.0 - B2);
+        const double S_hi = Sf * (1.0 + B2);
+        int first_below = K, first_amb = K;
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            if (s < nsk) {
+                const int i = s * WAVE + lane;
+                const bool valid = i < K;
+                const bool below = valid && (e[s] / S_lo < thr);
+                const bool above = valid && (e[s] / S_hi >= thr);
+                const uint64_t mb = ballot(below);
+                const uint64_t ma = ballot(valid && !below && !above);
+                if (mb && first_below == K) first_below = s * WAVE + __builtin_ctzll(mb);
+                if (ma && first_amb == K) first_amb = s * WAVE + __builtin_ctzll(ma);
+            }
+        }
+        if (first_amb < first_below) {
+            exact = true;
+        } else {
+            k0 = first_below;
+            S_used = Sf;
+        }
+    }
+    if (exact) {
+        const double S = exact_row_sum<T>(p, rowc, m, lane);
+        S_used = S;
+        k0 = K;
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            if (s < nsk) {
+                const int i = s * WAVE + lane;
+                const uint64_t mb = ballot(i < K && (e[s] / S < thr));
+                if (mb && k0 == K) k0 = s * WAVE + __builtin_ctzll(mb);
+            }
+        }
+    }
+    int k = k0 < 2 ? 2 : k0;
+    if (k > p.topk) k = p.topk;
+
+    // E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
+    double el = 0.0;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        if (s < nsk && i < k) el += e[s];
+    }
+    const double E = wave_sum_butterfly(el);
+
+    // q, inclusive prefix, overfill trim
+    int64_t cum[NSK];
+    int64_t carry = 0;
+    int kp = k;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        int64_t q = 0;
+        if (s < nsk && i < k) q = (int64_t)__builtin_rint((e[s] / E) * Rd);
+        int64_t c = (s < nsk) ? wave_incl_scan(q, lane) + carry : carry;
+        cum[s] = c;
+        if (s < nsk) {
+            carry = __shfl(c, WAVE - 1);
+            const uint64_t mo = ballot(i < k && c > (int64_t)R);
+            if (mo && kp == k) kp = s * WAVE + __builtin_ctzll(mo);
+        }
+    }
+    auto cum_at = [&](int i) -> int64_t {
+        int64_t val = 0;
+        const int si = i / WAVE, li = i % WAVE;
+#pragma unroll
+        for (int s = 0; s < NSK; ++s)
+            if (s == si) val = __shfl(cum[s], li);
+        return val;
+    };
+    const int64_t shift = (int64_t)R - cum_at(kp - 1) + (int64_t)st.lo;  // deficit + lo
+
+    // selection
+    int sel = -1;
+    uint32_t err = 0;
+    int32_t token = -1;
+    if (!DECODE) {
+        const int64_t bp = st.bit_pos + lane;
+        uint32_t bit = 0;
+        if (lane < p.P && bp < nbits) {
+            const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
+            bit = (pl[bp >> 3] >> (bp & 7)) & 1u;
+        }
+        const uint64_t mbits = ballot(bit != 0u);
+        const uint64_t idx = __builtin_bitreverse64(mbits) >> (64 - p.P);
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            if (s < nsk) {
+                const int i = s * WAVE + lane;
+                const uint64_t ms = ballot(i < kp && (uint64_t)(cum[s] + shift) > idx);
+                if (ms && sel < 0) sel = s * WAVE + __builtin_ctzll(ms);
+            }
+        }
+        if (sel < 0) err = NS_ST_ERR_RANGE;
+    } else {
+        const int32_t tok = p.in_token[b];
+        if (tok >= 0 && tok < V && !is_banned(p, tok)) {
+            const uint64_t kt = make_key(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+#pragma unroll
+            for (int s = 0; s < NSK; ++s) {
+                if (s < nsk) {
+                    const int i = s * WAVE + lane;
+                    const uint64_t ms = ballot(i < kp && sk[s] == kt);
+                    if (ms && sel < 0) sel = s * WAVE + __builtin_ctzll(ms);
+                }
+            }
+        }
+        if (sel < 0) err = NS_ST_ERR_DIVERGE;
+    }
+
+    if (sel >= 0) {
+        uint64_t tk = 0;
+        {
+            const int si = sel / WAVE, li = sel % WAVE;
+#pragma unroll
+            for (int s = 0; s < NSK; ++s)
+                if (s == si) tk = __shfl(sk[s], li);
+        }
+        token = (int32_t)key_id(tk);
+    }
+
+    // state update: cross-lane values are gathered by shuffles, every lane computes the same scalars
+    if (err == 0u) {
+        const int P = p.P;
+        const uint64_t mask = (P >= 64) ? ~0ull : ((1ull << P) - 1ull);
+        const uint64_t new_lo = sel > 0 ? (uint64_t)(cum_at(sel - 1) + shift) : st.lo;
+        const uint64_t new_hi = (uint64_t)(cum_at(sel) + shift);
+        const uint64_t top = new_hi - 1ull;
+        const uint64_t diff = (new_lo ^ top) & mask;
+        const int n = diff == 0ull ? P - 1 : P - (64 - __builtin_clzll(diff));
+        ns_stream_state ns = st;
+        if (DECODE) {
+            const bool last = p.is_last[b] != 0;
+            const int cntb = last ? P : n;
+            const uint64_t src = last ? new_lo : top;
+            if (lane == 0) {
+                uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
+                for (int t = 0; t < cntb; ++t) {
+                    const int64_t bp = st.bit_pos + t;
+                    const uint8_t bitv = (uint8_t)((src >> (P - 1 - t)) & 1u);
+                    const uint8_t bm = (uint8_t)(1u << (bp & 7));
+                    ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | bm) : (uint8_t)(ob[bp >> 3] & ~bm);
+                }
+            }
+            ns.bit_pos = st.bit_pos + cntb;
+        } else {
+            ns.bit_pos = st.bit_pos + n;
+        }
+        ns.lo = (new_lo << n) & mask;
+        ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
+        ns.ntokens = st.ntokens + 1;
+        ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
+        if (!DECODE && ns.bit_pos >= nbits) ns.flags |= NS_ST_DONE;
+        if (lane == 0) {
+            p.state[b] = ns;
+            if (!DECODE) {
+                p.out_token[b] = token;
+                if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+            }
+            if (p.trace) {
+                ns_step_trace tr;
+                tr.k = k;
+                tr.kprime = kp;
+                tr.sel = sel;
+                tr.n = n;
+                tr.token = token;
+                tr.exact = exact ? 1 : 0;
+                tr.S = S_used;
+                p.trace[b] = tr;
+            }
+        }
+    } else if (lane == 0) {
+        p.state[b].flags = st.flags | err | NS_ST_DONE;
+        if (p.trace) {
+            ns_step_trace tr;
+            tr.k = k;
+            tr.kprime = kp;
+            tr.sel = -1;
+            tr.n = -1;
+            tr.token = -1;
+            tr.exact = exact ? 1 : 0;
+            tr.S = S_used;
+            p.trace[b] = tr;
+        }
+    }
+    if (lane == 0 && p.counters) {
+        atomicAdd(&p.counters[0], 1ull);
+        if (exact) atomicAdd(&p.counters[1], 1ull);
+        if (ncompact) atomicAdd(&p.counters[2], (unsigned long long)ncompact);
+    }
+}
+
+__global__ void init_state_kernel(ns_stream_state* st, int B, int P) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) {
+        ns_stream_state s;
+        s.lo = 0;
+        s.hi = 1ull << P;
+        s.bit_pos = 0;
+        s.ntokens = 0;
+        s.flags = 0;
+        st[b] = s;
+    }
+}
+
+}  // namespace nsg
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+struct ns_ctx {
+    int device;
+    int max_batch;
+    int vocab;
+    int max_k;
+    int precision;
+    int dtype;
+    unsigned long long* d_counters;
+    std::string err;
+};
+
+static thread_local std::string g_err;
+
+static int fail(ns_ctx* ctx, int code, const std::string& msg) {
+    if (ctx)
+        ctx->err = msg;
+    else
+        g_err = msg;
+    return code;
+}
+
+extern "C" {
+
+const char* ns_version(void) { return "nsgcoder 0.1 gfx950"; }
+
+int ns_max_topk(int logits_dtype) {
+    const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
+    return nsg::CAND - TS;
+}
+
+const char* ns_last_error(const ns_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision, int logits_dtype) {
+    if (max_batch < 1 || vocab < 2 || max_k < 1 || precision < 1 || precision > 60 ||
+        (logits_dtype != NS_DTYPE_F32 && logits_dtype != NS_DTYPE_F16)) {
+        fail(nullptr, NS_ERR_CONFIG, "ns_create: invalid argument");
+        return nullptr;
+    }
+    if (max_k > ns_max_topk(logits_dtype)) {
+        fail(nullptr, NS_ERR_UNSUPPORTED, "ns_create: max_k exceeds the single-pass kernel limit");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        fail(nullptr, NS_ERR_HIP, "ns_create: hipSetDevice failed");
+        return nullptr;
+    }
+    ns_ctx* ctx = new ns_ctx();
+    ctx->device = device;
+    ctx->max_batch = max_batch;
+    ctx->vocab = vocab;
+    ctx->max_k = max_k;
+    ctx->precision = precision;
+    ctx->dtype = logits_dtype;
+    ctx->d_counters = nullptr;
+    if (hipMalloc((void**)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
+        delete ctx;
+        return nullptr;
+    }
+    return ctx;
+}
+
+void ns_destroy(ns_ctx* ctx) {
+    if (!ctx) return;
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    delete ctx;
+}
+
+int ns_init_state(ns_ctx* ctx, ns_stream_state* d_state, int B, void* hip_stream) {
+    if (!ctx || !d_state || B < 1 || B > ctx->max_batch) return fail(ctx, NS_ERR_CONFIG, "ns_init_state: bad argument");
+    const int threads = 256;
+    hipLaunchKernelGGL(nsg::init_state_kernel, dim3((B + threads - 1) / threads), dim3(threads), 0,
+                       (hipStream_t)hip_stream, d_state, B, ctx->precision);
+    if (hipGetLastError() != hipSuccess) return fail(ctx, NS_ERR_HIP, "ns_init_state: launch failed");
+    return NS_OK;
+}
+
+static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_t ld, int B, double temp,
+                   int topk, const int32_t* banned, int nbanned, ns_step_trace* d_trace, uint32_t flags,
+                   ns_stream_state* d_state) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
+    const int W = ctx->dtype == NS_DTYPE_F16 ? 8 : 4;
+    const int esz = ctx->dtype == NS_DTYPE_F16 ? 2 : 4;
+    if (!d_logits || !d_state || B < 1 || B > ctx->max_batch) return fail(ctx, NS_ERR_CONFIG, "bad batch or pointer");
+    if (ld < ctx->vocab || (ld % W) != 0) return fail(ctx, NS_ERR_CONFIG, "ld must be >= vocab and a multiple of 16 bytes");
+    if (((uintptr_t)d_logits & 15u) != 0u) return fail(ctx, NS_ERR_CONFIG, "logits must be 16-byte aligned");
+    if (!(temp > 0.0)) return fail(ctx, NS_ERR_CONFIG, "temperature must be positive");
+    if (topk < 1) return fail(ctx, NS_ERR_CONFIG, "topk must be positive");
+    if (nbanned < 0 || nbanned > NS_MAX_BANNED || (nbanned > 0 && !banned))
+        return fail(ctx, NS_ERR_CONFIG, "too many banned ids");
+    int ban[NS_MAX_BANNED];
+    int nb = 0;
+    for (int i = 0; i < nbanned; ++i)
+        if (banned[i] >= 0 && banned[i] < ctx->vocab) ban[nb++] = banned[i];
+    std::sort(ban, ban + nb);
+    nb = (int)(std::unique(ban, ban + nb) - ban);
+    const int nvalid = ctx->vocab - nb;
+    if (nvalid < 2) return fail(ctx, NS_ERR_CONFIG, "fewer than two valid token ids");
+    const int K = std::min(topk, nvalid);
+    if (K > ns_max_topk(ctx->dtype))
+        return fail(ctx, NS_ERR_UNSUPPORTED, "topk beyond the single-pass kernel limit (ns_max_topk)");
+    memset(&p, 0, sizeof p);
+    p.logits = d_logits;
+    p.ld = ld;
+    p.B = B;
+    p.V = ctx->vocab;
+    p.P = ctx->precision;
+    p.topk = topk;
+    p.K = K;
+    p.inv_temp = 1.0 / temp;
+    p.c32 = (float)(p.inv_temp * 1.4426950408889634);
+    p.nbanned = nb;
+    for (int i = 0; i < nb; ++i) p.banned[i] = ban[i];
+    p.flags = flags;
+    p.state = d_state;
+    p.trace = d_trace;
+    p.counters = ctx->d_counters;
+    (void)esz;
+    return NS_OK;
+}
+
+int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const uint8_t* d_payload,
+                   int64_t payload_stride, const int64_t* d_payload_nbits, ns_stream_state* d_state,
+                   int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride, double temp, int topk,
+                   const int32_t* banned, int nbanned, ns_step_trace* d_trace, uint32_t step_flags,
+                   void* hip_stream) {
+    nsg::StepParams p;
+    int rc = prepare(ctx, p, d_logits, ld, B, temp, topk, banned, nbanned, d_trace, step_flags, d_state);
+    if (rc != NS_OK) return rc;
+    if (!d_payload || !d_payload_nbits || !d_out_token || payload_stride < 0)
+        return fail(ctx, NS_ERR_CONFIG, "ns_encode_step: null payload/out pointer");
+    p.payload = d_payload;
+    p.payload_stride = payload_stride;
+    p.nbits = d_payload_nbits;
+    p.out_token = d_out_token;
+    p.hist = d_token_hist;
+    p.hist_stride = d_token_hist ? hist_stride : 0;
+    const dim3 grid((B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
+    if (ctx->dtype == NS_DTYPE_F16)
+        hipLaunchKernelGGL((nsg::coder_step_kernel<_Float16, false>), grid, block, 0, (hipStream_t)hip_stream, p);
+    else
+        hipLaunchKernelGGL((nsg::coder_step_kernel<float, false>), grid, block, 0, (hipStream_t)hip_stream, p);
+    if (hipGetLastError() != hipSuccess) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
+    return NS_OK;
+}
+
+int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const int32_t* d_in_token,
+                   const uint8_t* d_is_last, const uint8_t* d_active, ns_stream_state* d_state,
+                   uint8_t* d_out_bits, int64_t out_stride, double temp, int topk, const int32_t* banned,
+                   int nbanned, ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream) {
+    nsg::StepParams p;
+    int rc = prepare(ctx, p, d_logits, ld, B, temp, topk, banned, nbanned, d_trace, step_flags, d_state);
+    if (rc != NS_OK) return rc;
+    if (!d_in_token || !d_is_last || !d_out_bits || out_stride < 1)
+        return fail(ctx, NS_ERR_CONFIG, "ns_decode_step: null token/out pointer");
+    p.in_token = d_in_token;
+    p.is_last = d_is_last;
+    p.active = d_active;
+    p.out_bits = d_out_bits;
+    p.out_stride = out_stride;
+    const dim3 grid((B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
+    if (ctx->dtype == NS_DTYPE_F16)
+        hipLaunchKernelGGL((nsg::coder_step_kernel<_Float16, true>), grid, block, 0, (hipStream_t)hip_stream, p);
+    else
+        hipLaunchKernelGGL((nsg::coder_step_kernel<float, true>), grid, block, 0, (hipStream_t)hip_stream, p);
+    if (hipGetLastError() != hipSuccess) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
+    return NS_OK;
+}
+
+int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters3) {
+    if (!ctx || !host_counters3) return fail(ctx, NS_ERR_CONFIG, "ns_read_counters: bad argument");
+    unsigned long long h[4];
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h, ctx->d_counters, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(ctx, NS_ERR_HIP, "ns_read_counters: copy failed");
+    for (int i = 0; i < 3; ++i) host_counters3[i] = h[i];
+    return NS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+"""CPU: the C-ABI library loads and exports every entry point include/nsg_coder.h declares."""
+
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from neuralsteganography_amd import _lib
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "nsg_coder.h"
+
+
+def declared_symbols():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(ns_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    assert set(_lib.EXPORTS) == set(syms), syms
+
+
+def test_library_exports_every_declared_symbol():
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("libnsgcoder.so not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(str(_lib.LIB_PATH))
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+    assert _lib.version().startswith("nsgcoder")
+    assert _lib.max_topk(_lib.NS_DTYPE_F32) >= 300
+    assert _lib.max_topk(_lib.NS_DTYPE_F16) >= 300
+
+
+def test_struct_layouts_match_header():
+    assert ctypes.sizeof(_lib.NsStreamState) == 32
+    assert ctypes.sizeof(_lib.NsStepTrace) == 32
+    assert _lib.NsStreamState.bit_pos.offset == 16 and _lib.NsStreamState.flags.offset == 28
+    assert _lib.NsStepTrace.S.offset == 24
+
+
+def test_no_gpu_means_loud_failure():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from neuralsteganography_amd.coder import CoderContext, CoderParams
+
+    with pytest.raises(_lib.NativeLibraryError):
+        CoderContext(CoderParams(vocab=50257), max_batch=4)
