@@ -145,8 +145,10 @@ def main():
     f1 = sess.fields()
     c1 = ctx.counters()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    stream_steps = c1[0] - c0[0]
-    exact_steps = c1[1] - c0[1]
+    stream_steps = int(f1["ntokens"].sum() - f0["ntokens"].sum())
+    exact_steps = c1[0] - c0[0]
+    overflow_compactions = c1[1] - c0[1]
+    spec_misses = c1[2] - c0[2]
     bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
     sess.raise_errors()
 
@@ -191,6 +193,8 @@ def main():
         "bits_per_token": bits_all / max(ss_all, 1.0),
         "kernel_ms_avg": kern_ms,
         "exact_sum_fraction": exact_steps / max(stream_steps, 1),
+        "overflow_compactions_per_stream_step": overflow_compactions / max(stream_steps, 1),
+        "speculation_miss_fraction": spec_misses / max(stream_steps, 1),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": args.traffic_bytes,
                      "kernel": "coder_step_kernel<float,false>", "alg_bytes_per_launch": alg_bytes},

@@ -54,6 +54,10 @@ extern "C" {
 
 /* step flags */
 #define NS_STEP_FORCE_EXACT_SUM 1u /* always take the exact-sum path (parity testing) */
+/* diagnostic flags for phase timing only: the step does NOT advance any state when one is set */
+#define NS_STEP_DIAG_STREAM_ONLY 2u    /* stop after the streaming pass                           */
+#define NS_STEP_DIAG_NO_CANDIDATES 4u  /* streaming pass without candidate collection, then stop  */
+#define NS_STEP_DIAG_SKIP_CDF 8u       /* stop after the exact top-K ranking                      */
 
 #define NS_MAX_BANNED 8
 
@@ -111,9 +115,10 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
                    uint8_t* d_out_bits, int64_t out_stride, double temp, int topk, const int32_t* banned,
                    int nbanned, ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
 
-/* Diagnostics: counters[0] = stream-steps run, counters[1] = stream-steps that took the exact-sum path,
- * counters[2] = candidate-buffer compactions.  Synchronises the device. */
-int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters3);
+/* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
+ * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
+ * (row re-read), counters[3] = reserved.  Synchronises the device. */
+int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters4);
 
 #ifdef __cplusplus
 }

@@ -8,15 +8,20 @@ coder entry point fails loudly.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 LIB_PATH = PKG / "_build" / "libnsgcoder.so"
+# tools/ may point at an alternative build of the SAME source (compile-time tuning variants)
+if os.environ.get("NSG_CODER_LIB"):
+    LIB_PATH = Path(os.environ["NSG_CODER_LIB"]).resolve()
 
 NS_OK, NS_ERR_CONFIG, NS_ERR_UNSUPPORTED, NS_ERR_HIP = 0, -1, -2, -3
 NS_DTYPE_F32, NS_DTYPE_F16 = 0, 1
 NS_ST_DONE, NS_ST_ERR_RANGE, NS_ST_ERR_DIVERGE, NS_ST_EXACT_SUM = 1, 2, 4, 8
 NS_STEP_FORCE_EXACT_SUM = 1
+NS_STEP_DIAG_STREAM_ONLY, NS_STEP_DIAG_NO_CANDIDATES, NS_STEP_DIAG_SKIP_CDF = 2, 4, 8
 NS_MAX_BANNED = 8
 
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",

@@ -121,7 +121,7 @@ class CoderContext:
             raise _lib.NativeLibraryError(f"{what}: rc={rc}: {msg}")
 
     def counters(self) -> List[int]:
-        out = (ctypes.c_uint64 * 3)()
+        out = (ctypes.c_uint64 * 4)()
         self.check(_lib.lib().ns_read_counters(self._h, out), "ns_read_counters")
         return [int(v) for v in out]
 
@@ -182,11 +182,13 @@ class EncodeSession:
         self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
         return self.trace
 
-    def step(self, logits, *, force_exact: bool = False):
-        """One coder step on ``logits`` ([B, ld] contiguous rows, ld = :func:`row_stride`)."""
+    def step(self, logits, *, force_exact: bool = False, diag_flags: int = 0):
+        """One coder step on ``logits`` ([B, ld] contiguous rows, ld = :func:`row_stride`).
+
+        ``diag_flags`` (NS_STEP_DIAG_*) are for phase timing only: such a step advances no state."""
         p = self.ctx.params
         self._check_logits(logits)
-        flags = _lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0
+        flags = (_lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0) | int(diag_flags)
         rc = _lib.lib().ns_encode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
             _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), self.hist.shape[1],

@@ -33,10 +33,24 @@
 
 namespace nsg {
 
+#ifndef NSG_WPB
+#define NSG_WPB 4
+#endif
+#ifndef NSG_CAND
+#define NSG_CAND 1024
+#endif
+#ifndef NSG_PREFETCH
+#define NSG_PREFETCH 8
+#endif
+#ifndef NSG_MIN_WAVES_PER_EU
+#define NSG_MIN_WAVES_PER_EU 4
+#endif
+
 constexpr int WAVE = 64;
-constexpr int WPB = 4;        // waves (streams) per workgroup
-constexpr int CAND = 1024;    // candidate keys per wave (8 KiB LDS)
-constexpr int PREFETCH = 4;   // tiles in flight per wave
+#define NS_COUNTER_SHARDS 256
+constexpr int WPB = NSG_WPB;            // waves (streams) per workgroup
+constexpr int CAND = NSG_CAND;          // candidate keys per wave (8 B each, LDS)
+constexpr int PREFETCH = NSG_PREFETCH;  // tiles in flight per wave
 
 // ------------------------------------------------------------------------------------------------
 // canonical float64 exp -- identical operation sequence to or_exp_canon (oracle/nsg_oracle.c)
@@ -162,6 +176,7 @@ struct StepParams {
     float c32;  // (float)(inv_temp * log2(e))
     int nbanned;
     int banned[NS_MAX_BANNED];  // sorted ascending, unique, in [0, V)
+    int spec_j;  // speculative threshold rank in the 1024-id sample (0: no sample)
     uint32_t flags;
     // encode
     const uint8_t* payload;
@@ -191,7 +206,7 @@ __device__ __forceinline__ bool is_banned(const StepParams& p, int j) {
 
 // exact canonical row sum (oracle or_row_sum): id j -> lane (j>>2)&63, per-lane increasing, butterfly
 template <typename T>
-__device__ __noinline__ double exact_row_sum(const StepParams& p, const void* row, double m, int lane) {
+__device__ __forceinline__ double exact_row_sum(const StepParams& p, const void* row, double m, int lane) {
     double acc = 0.0;
     const int ngroups = (p.V + 3) >> 2;
     for (int g = lane; g < ngroups; g += WAVE) {
@@ -264,18 +279,99 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, int cnt, int K, in
     return kappa;
 }
 
-template <typename T, bool DECODE>
-__global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
+// buffer-resource row reader: one SRD per wave (uniform), range-checked 16-byte loads (0 beyond the row)
+__device__ __forceinline__ const void* uniform_ptr(const void* ptr) {
+    const uint64_t a = (uint64_t)ptr;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (const void*)(((uint64_t)hi << 32) | lo);
+}
+
+struct RowReader {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ RowReader(const void* base, uint32_t bytes)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), (short)0,
+                                               (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000)) {}
+    __device__ __forceinline__ uint4 vec(int v) const {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, 0);
+        return make_uint4(r[0], r[1], r[2], r[3]);
+    }
+};
+
+// Candidate buffer of one wave: keys of every element > thr seen so far (a superset of the running top-K).
+struct Cand {
+    uint64_t* keys;
+    int cnt;
+    int ncompact;
+    float thr;  // element passes iff x > thr
+};
+
+template <int W>
+__device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int K, int lane) {
+    float mx = x[0];
+#pragma unroll
+    for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+    if (!ballot(mx > c.thr)) return;
+    uint64_t msk[W];
+    int npt = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        msk[q] = ballot(x[q] > c.thr);
+        npt += popc64(msk[q]);
+    }
+    if (c.cnt + npt > CAND) {  // cnt > CAND - TS >= K: keep the exact running top-K
+        const uint64_t kappa = compact_topk(c.keys, c.cnt, K, lane);
+        ++c.ncompact;
+        c.cnt = K;
+        // later elements have larger ids than every buffered key, so ties at the K-th value rank below it
+        c.thr = key_val(kappa);
+        npt = 0;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            msk[q] = ballot(x[q] > c.thr);
+            npt += popc64(msk[q]);
+        }
+    }
+    int base = c.cnt;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        if (x[q] > c.thr) c.keys[base + lanes_below(msk[q])] = make_key(x[q], (uint32_t)(j0 + q));
+        base += popc64(msk[q]);
+    }
+    c.cnt = base;
+}
+
+// -inf for ids >= V (last tile only) and for banned ids (sorted; `bi`/`next_ban` advance monotonically)
+template <int W>
+__device__ __forceinline__ void mask_tile(const StepParams& p, float (&x)[W], int tile, int ntiles, int j0,
+                                          int& bi, int& next_ban) {
+    constexpr int TS = WAVE * W;
+    if (tile == ntiles - 1) {
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            if (j0 + q >= p.V) x[q] = -__builtin_inff();
+    }
+    const int tile_end = (tile + 1) * TS;
+    while (next_ban < tile_end) {  // wave-uniform, at most nbanned times per row
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            if (j0 + q == next_ban) x[q] = -__builtin_inff();
+        ++bi;
+        next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+    }
+}
+
+template <typename T, bool DECODE, int NSK>
+__global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_kernel(StepParams p) {
     constexpr int W = Elem<T>::W;
-    constexpr int TS = WAVE * W;               // elements per tile
-    constexpr int NSK = (CAND - TS) / WAVE;    // sorted-rank slots per lane (K <= CAND - TS)
+    constexpr int TS = WAVE * W;  // elements per tile (one 16-byte load per lane)
+    static_assert(NSK * WAVE <= CAND - TS, "K must leave room for one tile of appends");
     __shared__ uint64_t s_keys[WPB][CAND];
 
     const int lane = threadIdx.x & (WAVE - 1);
-    const int wv = threadIdx.x / WAVE;
-    const int b = blockIdx.x * WPB + wv;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + wv);
     if (b >= p.B) return;
-    uint64_t* keys = s_keys[wv];
 
     ns_stream_state st = p.state[b];
     if (st.flags & NS_ST_DONE) return;
@@ -290,126 +386,151 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
         if (p.active && !p.active[b]) return;
     }
 
-    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
-    const uint4* rowv = (const uint4*)rowc;
     const int V = p.V;
-    const int nvec = (V + W - 1) / W;
-    const int ntiles = (nvec + WAVE - 1) / WAVE;
+    const int K = p.K;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int ntiles = (V + TS - 1) / TS;
+    const float c32 = p.c32;
 
-    // ---------------- streaming pass ----------------
-    float tau = -__builtin_inff();
-    int cnt = 0;
-    int ncompact = 0;
+    Cand cand;
+    cand.keys = s_keys[wv];
+    cand.cnt = 0;
+    cand.ncompact = 0;
+    cand.thr = -__builtin_inff();
+    int nfallback = 0;
+
+    // ---------------- prologue: stratified sample -> softmax reference r and speculative threshold -----
+    // 16 blocks of 64 ids spread over the row (16 values per lane).  r = sample max (fast-sum reference);
+    // thr = the spec_j-th largest sample value (16-bit prefix), a GUESS verified at the end of the row.
     float r = 0.0f;
+    bool spec = false;
+    if (p.spec_j > 0) {
+        constexpr int LPB = WAVE / W;  // lanes per 64-id block
+        constexpr int NLD = 16 / W;    // sample loads per lane
+        float sv[16];
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int blk = i * W + lane / LPB;
+            const int jb = ((int)(((int64_t)blk * V) / 16) / W) * W + (lane % LPB) * W;
+            float x[W];
+            Elem<T>::unpack(rd.vec(jb / W), x);
+#pragma unroll
+            for (int q = 0; q < W; ++q) sv[i * W + q] = is_banned(p, jb + q) ? -__builtin_inff() : x[q];
+        }
+        float mx = sv[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, sv[i]);
+        r = wave_max(mx);
+        if (r == -__builtin_inff()) r = 0.0f;
+        uint32_t pre = 0;
+        for (int bit = 31; bit >= 16; --bit) {
+            const uint32_t c = pre | (1u << bit);
+            int n = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) n += popc64(ballot(ord32(sv[i]) >= c));
+            if (n >= p.spec_j) pre = c;
+        }
+        if (pre > 0x00800000u) {  // above ord(-inf): a finite threshold
+            cand.thr = unord32(pre - 1u);  // x > thr  <=>  ord(x) >= pre
+            spec = true;
+        }
+    }
+    if (p.flags & NS_STEP_DIAG_NO_CANDIDATES) cand.thr = __builtin_inff();
+
+    // ---------------- streaming pass (the HBM-bound part) ----------------
     double acc64 = 0.0;
     int bi = 0;
     int next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
-    const float c32 = p.c32;
-
     uint4 buf[PREFETCH];
 #pragma unroll
-    for (int d = 0; d < PREFETCH; ++d) {
-        const int v = d * WAVE + lane;
-        buf[d] = (d < ntiles && v < nvec) ? rowv[v] : make_uint4(0u, 0u, 0u, 0u);
+    for (int d = 0; d < PREFETCH; ++d) buf[d] = rd.vec(d * WAVE + lane);
+    if (p.spec_j <= 0) {  // no sample (small vocab): reference = max of the first tile
+        float x[W];
+        Elem<T>::unpack(buf[0], x);
+        int bi0 = 0, nb0 = next_ban;
+        mask_tile<W>(p, x, 0, ntiles, lane * W, bi0, nb0);
+        float mx = x[0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+        r = wave_max(mx);
+        if (r == -__builtin_inff()) r = 0.0f;
     }
-
-    for (int t0 = 0; t0 < ntiles; t0 += PREFETCH) {
-        uint4 nxt[PREFETCH];
+    auto process = [&](float (&x)[W], int tile) {
+        const int j0 = (tile * WAVE + lane) * W;
+        mask_tile<W>(p, x, tile, ntiles, j0, bi, next_ban);
+        float a = 0.0f;
+#pragma unroll
+        for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((x[q] - r) * c32);
+        acc64 += (double)a;
+        offer<W>(cand, x, j0, K, lane);
+    };
+    // Full groups: every slot is consumed, then refilled PREFETCH tiles ahead into the same registers
+    // (no copies, so the per-tile wait is a counted vmcnt, never a drain).  Loads past the row are
+    // range-checked by the buffer descriptor and return zeros.
+    int tile = 0;
+    for (; tile + PREFETCH <= ntiles; tile += PREFETCH) {
 #pragma unroll
         for (int d = 0; d < PREFETCH; ++d) {
-            const int v = (t0 + PREFETCH + d) * WAVE + lane;
-            nxt[d] = (t0 + PREFETCH + d < ntiles && v < nvec) ? rowv[v] : make_uint4(0u, 0u, 0u, 0u);
+            float x[W];
+            Elem<T>::unpack(buf[d], x);
+            process(x, tile + d);
+            buf[d] = rd.vec((tile + d + PREFETCH) * WAVE + lane);
         }
+    }
 #pragma unroll
-        for (int d = 0; d < PREFETCH; ++d) {
-            const int tile = t0 + d;
-            if (tile < ntiles) {
-                const int v = tile * WAVE + lane;
-                const int j0 = v * W;
-                float x[W];
-                Elem<T>::unpack(buf[d], x);
-#pragma unroll
-                for (int q = 0; q < W; ++q)
-                    if (j0 + q >= V) x[q] = -__builtin_inff();
-                const int tile_end = (tile + 1) * TS;
-                while (next_ban < tile_end) {  // wave-uniform, rare
-#pragma unroll
-                    for (int q = 0; q < W; ++q)
-                        if (j0 + q == next_ban) x[q] = -__builtin_inff();
-                    ++bi;
-                    next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
-                }
-                if (tile == 0) {
-                    float mx = x[0];
-#pragma unroll
-                    for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
-                    r = wave_max(mx);
-                    if (r == -__builtin_inff()) r = 0.0f;
-                }
-                // softmax denominator estimate (fast path)
-                float a = 0.0f;
-#pragma unroll
-                for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((x[q] - r) * c32);
-                acc64 += (double)a;
-                // candidates
-                float mx = x[0];
-#pragma unroll
-                for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
-                if (ballot(mx > tau)) {
-                    uint64_t msk[W];
-                    int npt = 0;
-#pragma unroll
-                    for (int q = 0; q < W; ++q) {
-                        msk[q] = ballot(x[q] > tau);
-                        npt += popc64(msk[q]);
-                    }
-                    if (cnt + npt > CAND) {
-                        const uint64_t kappa = compact_topk(keys, cnt, p.K, lane);
-                        ++ncompact;
-                        cnt = p.K;
-                        tau = unord32((uint32_t)(kappa >> 32));
-                        npt = 0;
-#pragma unroll
-                        for (int q = 0; q < W; ++q) {
-                            msk[q] = ballot(x[q] > tau);
-                            npt += popc64(msk[q]);
-                        }
-                    }
-                    int base = cnt;
-#pragma unroll
-                    for (int q = 0; q < W; ++q) {
-                        if (x[q] > tau) keys[base + lanes_below(msk[q])] = make_key(x[q], (uint32_t)(j0 + q));
-                        base += popc64(msk[q]);
-                    }
-                    cnt = base;
-                }
-            }
+    for (int d = 0; d < PREFETCH; ++d) {
+        if (tile + d < ntiles) {
+            float x[W];
+            Elem<T>::unpack(buf[d], x);
+            process(x, tile + d);
         }
-#pragma unroll
-        for (int d = 0; d < PREFETCH; ++d) buf[d] = nxt[d];
+    }
+    // speculation check: the buffer holds the true top-K iff at least K elements passed the guess
+    // (or a compaction happened, which needs > CAND - TS >= K passes).  Else re-stream, exactly.
+    if (spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) {
+        ++nfallback;
+        cand.cnt = 0;
+        cand.thr = -__builtin_inff();
+        int bj = 0, nbj = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        for (int tile = 0; tile < ntiles; ++tile) {
+            float x[W];
+            Elem<T>::unpack(rd.vec(tile * WAVE + lane), x);
+            const int j0 = (tile * WAVE + lane) * W;
+            mask_tile<W>(p, x, tile, ntiles, j0, bj, nbj);
+            offer<W>(cand, x, j0, K, lane);
+        }
     }
     lds_fence();
+    if (p.flags & (NS_STEP_DIAG_STREAM_ONLY | NS_STEP_DIAG_NO_CANDIDATES)) {  // diagnostic timing only
+        const double s_r = wave_sum_butterfly(acc64);
+        if (lane == 0 && p.trace) p.trace[b].S = s_r + (double)cand.cnt + (double)cand.ncompact;
+        return;
+    }
 
     // ---------------- exact top-K, ranked ----------------
-    const int K = p.K;
-    if (cnt > K) {
-        compact_topk(keys, cnt, K, lane);
-        ++ncompact;
-    }
+    uint64_t* keys = cand.keys;
+    if (cand.cnt > K) compact_topk(keys, cand.cnt, K, lane);
+    const int nsk = (K + WAVE - 1) / WAVE;
+    const int K8 = (K + 7) & ~7;
+    if (lane < K8 - K) keys[K + lane] = 0ull;  // zero pad: never counted as greater
+    lds_fence();
     uint64_t sk[NSK];
     int rk[NSK];
-    const int nsk = (K + WAVE - 1) / WAVE;
 #pragma unroll
     for (int s = 0; s < NSK; ++s) {
         const int i = s * WAVE + lane;
         sk[s] = (s < nsk && i < K) ? keys[i] : 0ull;
         rk[s] = 0;
     }
-    for (int t = 0; t < K; ++t) {
-        const uint64_t o = keys[t];  // LDS broadcast
+    for (int t = 0; t < K8; t += 8) {
+        uint64_t o[8];
 #pragma unroll
-        for (int s = 0; s < NSK; ++s)
-            if (s < nsk) rk[s] += (o > sk[s]) ? 1 : 0;
+        for (int u = 0; u < 8; ++u) o[u] = keys[t + u];  // LDS broadcast reads, 8 in flight
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int s = 0; s < NSK; ++s) rk[s] += (o[u] > sk[s]) ? 1 : 0;
     }
     lds_fence();
 #pragma unroll
@@ -424,8 +545,13 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
         sk[s] = (s < nsk && i < K) ? keys[i] : 0ull;
     }
 
+    if (p.flags & NS_STEP_DIAG_SKIP_CDF) {
+        if (lane == 0 && p.trace) p.trace[b].S = (double)key_val(keys[0]) + (double)cand.ncompact;
+        return;
+    }
+
     // ---------------- CDF step (canonical float64) ----------------
-    const double m = (double)key_val(keys[0]);
+    const double m = (double)key_val(__shfl(sk[0], 0));
     double e[NSK];
 #pragma unroll
     for (int s = 0; s < NSK; ++s) {
@@ -441,7 +567,7 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
     const double t_m = (m - (double)r) * (double)c32;
     bool exact = (p.flags & NS_STEP_FORCE_EXACT_SUM) != 0u;
     exact = exact || !(S_r > 0.0 && S_r < 1.0e300) || !(t_m <= 100.0 && t_m >= -60.0);
-    double S_used;
+    double S_used = 0.0;
     int k0 = K;
     if (!exact) {
         const double f = exp_canon(((double)r - m) * p.inv_temp);
@@ -452,16 +578,17 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
                           + (double)(W + 1) * u24                                   // fp32 partials
                           + 1.0e-13;
         const double B2 = 2.0 * eb + 1.0e-12;
-        const double S_lo = Sf * (1.0 - B2);
-        const double S_hi = Sf * (1.0 + B2);
+        // reciprocals with an extra 1e-15 margin stand in for the per-element divisions
+        const double inv_lo = 1.0 / (Sf * (1.0 - B2) * (1.0 - 1.0e-15));
+        const double inv_hi = 1.0 / (Sf * (1.0 + B2) * (1.0 + 1.0e-15));
         int first_below = K, first_amb = K;
 #pragma unroll
         for (int s = 0; s < NSK; ++s) {
             if (s < nsk) {
                 const int i = s * WAVE + lane;
                 const bool valid = i < K;
-                const bool below = valid && (e[s] / S_lo < thr);
-                const bool above = valid && (e[s] / S_hi >= thr);
+                const bool below = valid && (e[s] * inv_lo < thr);
+                const bool above = valid && (e[s] * inv_hi >= thr);
                 const uint64_t mb = ballot(below);
                 const uint64_t ma = ballot(valid && !below && !above);
                 if (mb && first_below == K) first_below = s * WAVE + __builtin_ctzll(mb);
@@ -567,12 +694,10 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
 
     if (sel >= 0) {
         uint64_t tk = 0;
-        {
-            const int si = sel / WAVE, li = sel % WAVE;
+        const int si = sel / WAVE, li = sel % WAVE;
 #pragma unroll
-            for (int s = 0; s < NSK; ++s)
-                if (s == si) tk = __shfl(sk[s], li);
-        }
+        for (int s = 0; s < NSK; ++s)
+            if (s == si) tk = __shfl(sk[s], li);
         token = (int32_t)key_id(tk);
     }
 
@@ -640,10 +765,13 @@ __global__ __launch_bounds__(WPB* WAVE) void coder_step_kernel(StepParams p) {
             p.trace[b] = tr;
         }
     }
-    if (lane == 0 && p.counters) {
-        atomicAdd(&p.counters[0], 1ull);
-        if (exact) atomicAdd(&p.counters[1], 1ull);
-        if (ncompact) atomicAdd(&p.counters[2], (unsigned long long)ncompact);
+    // rare-event diagnostics only (no per-step atomics): sharded by block so waves never contend
+    const int overflow = cand.ncompact;
+    if (lane == 0 && p.counters && (exact || overflow > 0 || nfallback)) {
+        unsigned long long* c = p.counters + 4 * (blockIdx.x & (NS_COUNTER_SHARDS - 1));
+        if (exact) atomicAdd(&c[0], 1ull);
+        if (overflow > 0) atomicAdd(&c[1], (unsigned long long)overflow);
+        if (nfallback) atomicAdd(&c[2], (unsigned long long)nfallback);
     }
 }
 
@@ -686,6 +814,40 @@ static int fail(ns_ctx* ctx, int code, const std::string& msg) {
     return code;
 }
 
+template <typename T, bool DECODE, int NSK>
+static void launch_one(const nsg::StepParams& p, hipStream_t s) {
+    const dim3 grid((p.B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
+    hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK>), grid, block, 0, s, p);
+}
+
+template <typename T, bool DECODE>
+static void launch_t(const nsg::StepParams& p, hipStream_t s) {
+    // rank slots per lane from K (register footprint of the CDF tail)
+    if (p.K <= 128)
+        launch_one<T, DECODE, 2>(p, s);
+    else if (p.K <= 320)
+        launch_one<T, DECODE, 5>(p, s);
+    else if (p.K <= 512)
+        launch_one<T, DECODE, 8>(p, s);
+    else
+        launch_one<T, DECODE, (nsg::CAND - nsg::WAVE * 4) / nsg::WAVE>(p, s);
+}
+
+template <bool DECODE>
+static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
+    if (ctx->dtype == NS_DTYPE_F16) {
+        if (p.K <= 128)
+            launch_one<_Float16, DECODE, 2>(p, s);
+        else if (p.K <= 320)
+            launch_one<_Float16, DECODE, 5>(p, s);
+        else
+            launch_one<_Float16, DECODE, (nsg::CAND - nsg::WAVE * 8) / nsg::WAVE>(p, s);
+    } else {
+        launch_t<float, DECODE>(p, s);
+    }
+    return hipGetLastError() == hipSuccess;
+}
+
 extern "C" {
 
 const char* ns_version(void) { return "nsgcoder 0.1 gfx950"; }
@@ -719,8 +881,8 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->precision = precision;
     ctx->dtype = logits_dtype;
     ctx->d_counters = nullptr;
-    if (hipMalloc((void**)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
+    if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
         delete ctx;
         return nullptr;
@@ -780,6 +942,15 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     p.nbanned = nb;
     for (int i = 0; i < nb; ++i) p.banned[i] = ban[i];
     p.flags = flags;
+    // speculative candidate threshold: the spec_j-th largest of a 1024-id stratified sample, chosen so that
+    // about 3.2*K ids of the row pass it (a guess verified per row; a miss costs one extra row read)
+    p.spec_j = 0;
+    if (ctx->vocab >= 2048) {
+        const double j = 3.2 * (double)K * 1024.0 / (double)nvalid;
+        int sj = (int)j + 1;
+        if (sj < 16) sj = 16;
+        if (sj < 256) p.spec_j = sj;
+    }
     p.state = d_state;
     p.trace = d_trace;
     p.counters = ctx->d_counters;
@@ -803,12 +974,7 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
     p.out_token = d_out_token;
     p.hist = d_token_hist;
     p.hist_stride = d_token_hist ? hist_stride : 0;
-    const dim3 grid((B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
-    if (ctx->dtype == NS_DTYPE_F16)
-        hipLaunchKernelGGL((nsg::coder_step_kernel<_Float16, false>), grid, block, 0, (hipStream_t)hip_stream, p);
-    else
-        hipLaunchKernelGGL((nsg::coder_step_kernel<float, false>), grid, block, 0, (hipStream_t)hip_stream, p);
-    if (hipGetLastError() != hipSuccess) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
+    if (!launch<false>(ctx, p, (hipStream_t)hip_stream)) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
     return NS_OK;
 }
 
@@ -826,22 +992,19 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
     p.active = d_active;
     p.out_bits = d_out_bits;
     p.out_stride = out_stride;
-    const dim3 grid((B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
-    if (ctx->dtype == NS_DTYPE_F16)
-        hipLaunchKernelGGL((nsg::coder_step_kernel<_Float16, true>), grid, block, 0, (hipStream_t)hip_stream, p);
-    else
-        hipLaunchKernelGGL((nsg::coder_step_kernel<float, true>), grid, block, 0, (hipStream_t)hip_stream, p);
-    if (hipGetLastError() != hipSuccess) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
+    if (!launch<true>(ctx, p, (hipStream_t)hip_stream)) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
     return NS_OK;
 }
 
-int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters3) {
-    if (!ctx || !host_counters3) return fail(ctx, NS_ERR_CONFIG, "ns_read_counters: bad argument");
-    unsigned long long h[4];
+int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters4) {
+    if (!ctx || !host_counters4) return fail(ctx, NS_ERR_CONFIG, "ns_read_counters: bad argument");
+    unsigned long long h[4 * NS_COUNTER_SHARDS];
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h, ctx->d_counters, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(ctx, NS_ERR_HIP, "ns_read_counters: copy failed");
-    for (int i = 0; i < 3; ++i) host_counters3[i] = h[i];
+    for (int i = 0; i < 4; ++i) host_counters4[i] = 0;
+    for (int sh = 0; sh < NS_COUNTER_SHARDS; ++sh)
+        for (int i = 0; i < 4; ++i) host_counters4[i] += h[4 * sh + i];
     return NS_OK;
 }
 

@@ -173,3 +173,51 @@ def test_empty_and_single_bit_payloads():
         assert toks[s] == otoks
     out = decode_batch(ctx, toks[1:], _logits_fn(9, [1, 2], V, 3.0, "f32", row_stride(V, "f32")))
     assert out[0][:1] == [1] and out[1][:3] == [0, 1, 1]
+
+
+def _sample_ids(V, W=4):
+    ids = []
+    for blk in range(16):
+        start = ((blk * V) // 16) // W * W
+        ids.extend(range(start, start + 64))
+    return np.asarray(ids)
+
+
+@pytest.mark.parametrize("mode", ["miss", "overflow"])
+def test_adversarial_rows_exercise_fallback_paths(mode):
+    """Rows whose stratified sample is unrepresentative: 'miss' makes the speculative threshold too high
+    (the wave must re-read its row), 'overflow' makes it far too low (many compactions).  Tokens must
+    still match the oracle exactly."""
+    from neuralsteganography_amd.coder import CoderParams, EncodeSession, row_stride
+
+    torch = _torch()
+    V, B = 50257, 4
+    params = CoderParams(vocab=V, precision=26, temp=0.9, topk=300)
+    ctx = _ctx(params, B)
+    ld = row_stride(V, "f32")
+    samp = _sample_ids(V)
+
+    def row(s, t):
+        x = synthetic.logits_row(77, s, t, V, 1.0)
+        if mode == "miss":
+            x[samp] += 12.0
+        else:
+            x[samp] -= 12.0
+        return x.astype(np.float32)
+
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 8)) for s in range(B)]
+    expect = [oracle.encode_stream(lambda t, s=s: row(s, t), bits[s], banned=params.banned_ids(), temp=0.9,
+                                   precision=26, topk=300)[0] for s in range(B)]
+    sess = EncodeSession(ctx, bits)
+    c0 = ctx.counters()
+    for t in range(max(map(len, expect))):
+        arr = np.zeros((B, ld), np.float32)
+        for s in range(B):
+            arr[s, :V] = row(s, t)
+        sess.step(torch.from_numpy(arr).cuda())
+    c1 = ctx.counters()
+    assert sess.tokens() == expect
+    if mode == "miss":
+        assert c1[2] > c0[2], "speculation miss path was not exercised"
+    else:
+        assert c1[1] > c0[1], "overflow compaction path was not exercised"
