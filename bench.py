@@ -87,6 +87,23 @@ def cpu_baseline(pool_h, payload, nbits, args, seconds):
                       f"({dt:.1f} s on 1 core)"}
 
 
+def measured_traffic(args, version):
+    """Per-launch HBM bytes from a committed rocprofv3 PMC record (tools/pmc_traffic.py) of THIS library
+    build and workload, else None."""
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "pmc_traffic_*.json"))):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if (rec.get("library_version") == version and rec.get("batch") == args.batch and rec.get("vocab") == args.vocab
+                and rec.get("dtype") == args.dtype and rec.get("topk") == args.topk):
+            best = (rec["traffic_bytes_per_launch"], Path(path).name)
+    return best
+
+
 def main():
     args = parse()
     import torch
@@ -163,6 +180,11 @@ def main():
     else:
         bits_all, ss_all, elapsed_max, kern_ms_max = float(bits), float(stream_steps), elapsed, kern_ms
 
+    from neuralsteganography_amd import _lib
+
+    traffic = measured_traffic(args, _lib.version())
+    if args.traffic_bytes is not None:
+        traffic = (args.traffic_bytes, "command line")
     esz = 2 if args.dtype == "f16" else 4
     per_stream_step = V * esz + 76  # logit row + state r/w (64) + token (4) + history (4) + payload window (~4)
     alg_bytes = B * per_stream_step
@@ -196,7 +218,8 @@ def main():
         "overflow_compactions_per_stream_step": overflow_compactions / max(stream_steps, 1),
         "speculation_miss_fraction": spec_misses / max(stream_steps, 1),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": args.traffic_bytes,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None,
                      "kernel": "coder_step_kernel<float,false>", "alg_bytes_per_launch": alg_bytes},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

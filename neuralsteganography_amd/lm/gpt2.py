@@ -1,0 +1,198 @@
+"""Batched GPT-2 forward with a preallocated KV cache, writing logits straight into the coder's layout.
+
+This is the L1 "LM runtime" of SURVEY.md §1 rebuilt for batch B on PyTorch-ROCm (the GEMMs run on MFMA
+through rocBLAS/hipBLASLt; the coder step is the hand-written HIP kernel).  It reproduces the reference's
+forward semantics (``code_base/arithmetic.py:12-48,115-122``):
+
+* the first call runs the whole context with default positions ``0..T-1``;
+* every later call feeds ONE token per stream with ``position_ids = cache_len % n_positions``
+  (``_position_ids_for_cache``, ``:44-48``) and attends to the whole cache: the reference never truncates
+  it (``limit_past`` slices head_dim, a no-op, ``code_base/utils.py:19-30``).
+
+Logits are produced as ``h @ wte^T`` into a ``[B, ld]`` buffer with ``ld = row_stride(V)`` (zero weight
+columns beyond V), so the coder reads 16-byte-aligned rows without a copy.  Weights are taken from a
+Hugging Face ``GPT2LMHeadModel`` (pretrained when available offline, random-init otherwise).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from ..coder import row_stride
+
+
+@dataclass
+class GPT2Shape:
+    n_layer: int
+    n_head: int
+    n_embd: int
+    vocab: int
+    n_positions: int
+    eps: float
+
+
+class BatchedGPT2:
+    """GPT-2 decoder for B streams in lockstep.
+
+    ``compute_dtype`` is the weight/activation dtype (fp16 on the GPU by default); ``logits_dtype`` is what
+    the coder reads (``torch.float32`` or ``torch.float16``)."""
+
+    def __init__(self, hf_model, *, device=None, compute_dtype=None, logits_dtype=torch.float32):
+        cfg = hf_model.config
+        self.shape = GPT2Shape(cfg.n_layer, cfg.n_head, cfg.n_embd, cfg.vocab_size, cfg.n_positions,
+                               cfg.layer_norm_epsilon)
+        self.device = torch.device(device) if device is not None else next(hf_model.parameters()).device
+        if compute_dtype is None:
+            compute_dtype = torch.float16 if self.device.type == "cuda" else torch.float32
+        self.dtype = compute_dtype
+        self.logits_dtype = logits_dtype
+        self.ld = row_stride(self.shape.vocab, "f16" if logits_dtype == torch.float16 else "f32")
+        sd = {k: v.detach() for k, v in hf_model.state_dict().items()}
+        dev, dt = self.device, self.dtype
+
+        def w(name):
+            return sd[name].to(device=dev, dtype=dt).contiguous()
+
+        pre = "transformer."
+        self.wte = w(pre + "wte.weight")
+        self.wpe = w(pre + "wpe.weight")
+        self.layers = []
+        for i in range(self.shape.n_layer):
+            p = f"{pre}h.{i}."
+            self.layers.append({
+                "ln1_w": w(p + "ln_1.weight"), "ln1_b": w(p + "ln_1.bias"),
+                "qkv_w": w(p + "attn.c_attn.weight"), "qkv_b": w(p + "attn.c_attn.bias"),
+                "o_w": w(p + "attn.c_proj.weight"), "o_b": w(p + "attn.c_proj.bias"),
+                "ln2_w": w(p + "ln_2.weight"), "ln2_b": w(p + "ln_2.bias"),
+                "fc_w": w(p + "mlp.c_fc.weight"), "fc_b": w(p + "mlp.c_fc.bias"),
+                "pr_w": w(p + "mlp.c_proj.weight"), "pr_b": w(p + "mlp.c_proj.bias"),
+            })
+        self.lnf_w = w(pre + "ln_f.weight")
+        self.lnf_b = w(pre + "ln_f.bias")
+        # lm_head = wte^T padded to ld columns (zeros beyond V): logits land in the coder's row layout
+        head = torch.zeros((self.shape.n_embd, self.ld), device=dev, dtype=dt)
+        head[:, : self.shape.vocab] = self.wte.t()
+        self.head = head
+        self.B = 0
+        self.L = 0
+        self.k_cache = self.v_cache = None
+
+    # ------------------------------------------------------------------
+    def allocate(self, B: int, max_len: int) -> None:
+        s = self.shape
+        hd = s.n_embd // s.n_head
+        shp = (s.n_layer, B, s.n_head, max_len, hd)
+        self.k_cache = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        self.v_cache = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        self.B, self.L, self.max_len = B, 0, max_len
+
+    def grow(self, extra: int) -> None:
+        """Enlarge the KV cache by ``extra`` positions (copying the filled part); low-entropy streams can
+        need more tokens than the initial budget."""
+        s = self.shape
+        new_len = self.max_len + int(extra)
+        hd = s.n_embd // s.n_head
+        shp = (s.n_layer, self.B, s.n_head, new_len, hd)
+        k = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        v = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        k[:, :, :, : self.L] = self.k_cache[:, :, :, : self.L]
+        v[:, :, :, : self.L] = self.v_cache[:, :, :, : self.L]
+        self.k_cache, self.v_cache, self.max_len = k, v, new_len
+
+    def _ln(self, x, wgt, b):
+        return F.layer_norm(x, (self.shape.n_embd,), wgt, b, self.shape.eps)
+
+    def _block(self, i, h, positions_new: int, causal: bool):
+        s = self.shape
+        lw = self.layers[i]
+        B, T, C = h.shape
+        H, D = s.n_head, C // s.n_head
+        a = self._ln(h, lw["ln1_w"], lw["ln1_b"])
+        qkv = torch.addmm(lw["qkv_b"], a.reshape(B * T, C), lw["qkv_w"]).view(B, T, 3, H, D)
+        q = qkv[:, :, 0].transpose(1, 2)
+        k = qkv[:, :, 1].transpose(1, 2)
+        v = qkv[:, :, 2].transpose(1, 2)
+        L0 = self.L
+        self.k_cache[i, :B, :, L0:L0 + T] = k
+        self.v_cache[i, :B, :, L0:L0 + T] = v
+        kk = self.k_cache[i, :B, :, : L0 + T]
+        vv = self.v_cache[i, :B, :, : L0 + T]
+        if causal:
+            o = F.scaled_dot_product_attention(q, kk, vv, is_causal=True)
+        else:
+            o = F.scaled_dot_product_attention(q, kk, vv)
+        o = o.transpose(1, 2).reshape(B * T, C)
+        h = h + torch.addmm(lw["o_b"], o, lw["o_w"]).view(B, T, C)
+        m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
+        f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B * T, C), lw["fc_w"]), approximate="tanh")
+        h = h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, T, C)
+        return h
+
+    def _logits(self, h_last):
+        hf = self._ln(h_last, self.lnf_w, self.lnf_b)
+        out = hf @ self.head
+        return out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
+
+    @torch.no_grad()
+    def prefill(self, context: Sequence[int], B: int, max_new: int) -> torch.Tensor:
+        """Run the shared context once (reference: first call, default positions) and broadcast its cache
+        to B streams.  Returns the ``[B, ld]`` logits for the next token."""
+        ctx = [int(t) for t in list(context)[-1022:]]  # code_base/arithmetic.py:90
+        T = len(ctx)
+        if T < 1:
+            raise ValueError("context must contain at least one token")
+        if min(ctx) < 0 or max(ctx) >= self.shape.vocab:  # host check: never gather out of the table
+            raise ValueError(f"context token ids must lie in [0, {self.shape.vocab})")
+        self.allocate(B, T + max_new)
+        ids = torch.tensor([ctx], device=self.device, dtype=torch.long)
+        pos = torch.arange(T, device=self.device) % self.shape.n_positions
+        h = self.wte[ids] + self.wpe[pos][None]
+        # run the context for one stream, then copy its cache to every stream
+        self.B_run = 1
+        saveB = self.B
+        self.B = 1
+        for i in range(self.shape.n_layer):
+            h = self._block(i, h, T, causal=True)
+        self.B = saveB
+        for i in range(self.shape.n_layer):
+            self.k_cache[i, 1:B, :, :T] = self.k_cache[i, 0:1, :, :T]
+            self.v_cache[i, 1:B, :, :T] = self.v_cache[i, 0:1, :, :T]
+        self.L = T
+        lg = self._logits(h[:, -1])
+        return lg.expand(B, -1).contiguous()
+
+    @torch.no_grad()
+    def step(self, tokens: torch.Tensor) -> torch.Tensor:
+        """Feed one token per stream (``[B]`` int); position = cache length mod n_positions."""
+        B = self.B
+        if self.L >= self.max_len:
+            self.grow(max(64, self.max_len))
+        if tokens.shape != (B,):
+            raise ValueError(f"expected {B} tokens")
+        pos = self.L % self.shape.n_positions
+        h = (self.wte[tokens.long()] + self.wpe[pos])[:, None, :]
+        for i in range(self.shape.n_layer):
+            h = self._block(i, h, 1, causal=False)
+        self.L += 1
+        return self._logits(h[:, -1])
+
+
+def random_gpt2(name: str = "gpt2", *, seed: int = 1234, **overrides):
+    """Random-init GPT-2 of a named size (no network: the architecture only).  SURVEY.md §8(c)."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    sizes = {"gpt2": dict(n_layer=12, n_head=12, n_embd=768),
+             "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),
+             "tiny": dict(n_layer=2, n_head=2, n_embd=64)}
+    kw = dict(sizes[name])
+    kw.update(overrides)
+    torch.manual_seed(seed)
+    cfg = GPT2Config(**kw)
+    model = GPT2LMHeadModel(cfg)
+    model.eval()
+    return model

@@ -1,0 +1,75 @@
+"""CPU: batched GPT-2 forward vs Hugging Face (reference semantics incl. position wrap), provider registry,
+codec slot and quality mapping."""
+
+import copy
+
+import pytest
+import torch
+
+from neuralsteganography_amd.codec import api as codec_api
+from neuralsteganography_amd.exceptions import ConfigurationError
+from neuralsteganography_amd.lm import load_lm
+from neuralsteganography_amd.lm.arithmetic import ByteTokenizer, coder_params_from_quality
+from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+
+
+def test_batched_gpt2_matches_hf_with_position_wrap():
+    """code_base/arithmetic.py:44-48,115-122: one token per step, position = cache_len % n_positions, cache
+    never truncated.  fp32 tolerance 1e-5 absolute."""
+    m = random_gpt2("tiny", vocab_size=700, n_positions=16)
+    g = BatchedGPT2(m, device="cpu", compute_dtype=torch.float32)
+    ctx = [5, 7, 9, 11, 13]
+    B = 3
+    lg = g.prefill(ctx, B, 24)
+    with torch.no_grad():
+        out = m(torch.tensor([ctx]), use_cache=True)
+    assert (lg[0, :700] - out.logits[0, -1]).abs().max().item() < 1e-5
+    assert torch.all(lg[:, 700:] == 0)  # padded columns
+    pasts = [copy.deepcopy(out.past_key_values) for _ in range(B)]
+    gen = torch.Generator().manual_seed(0)
+    for t in range(20):  # 5 + 20 > n_positions = 16: exercises the wrap
+        tok = torch.randint(0, 700, (B,), generator=gen)
+        lg = g.step(tok)
+        for b in range(B):
+            L = pasts[b].get_seq_length()
+            with torch.no_grad():
+                o = m(tok[b].view(1, 1), past_key_values=pasts[b], use_cache=True,
+                      position_ids=torch.tensor([[L % 16]]))
+            pasts[b] = o.past_key_values
+            assert (lg[b, :700] - o.logits[0, -1]).abs().max().item() < 1e-5
+
+
+def test_registry_and_codec_slot_with_mock():
+    lm = load_lm("mock")
+    toks = codec_api.encode_arithmetic(b"hello stego", lm, quality={})
+    assert codec_api.decode_arithmetic(toks, lm, quality={}) == b"hello stego"
+    assert codec_api.encode_arithmetic(b"", lm, quality={}) == []
+    assert codec_api.decode_arithmetic([], lm, quality={}) == b""
+    with pytest.raises(ConfigurationError):
+        load_lm("no-such-model")
+
+
+def test_quality_mapping_follows_reference_defaults_and_aliases():
+    p = coder_params_from_quality({}, 50257, "f32")
+    assert (p.temp, p.precision, p.topk) == (1.0, 16, 50000)  # code_base/arithmetic.py:85-87
+    p = coder_params_from_quality({"temperature": 0.9, "top_k": 300, "precision": 26}, 50257, "f32")
+    assert (p.temp, p.precision, p.topk) == (0.9, 26, 300)
+    assert p.banned_ids() == [50256, 628]
+    with pytest.raises(ConfigurationError):
+        coder_params_from_quality({"temp": 0.0}, 50257, "f32")
+
+
+def test_byte_tokenizer_seed():
+    t = ByteTokenizer()
+    assert t.encode("<|endoftext|>") == [50256]
+    assert t.decode(t.encode("abc")) == "abc"
+    assert ByteTokenizer(2000).encode("<|endoftext|>") == [1999]
+
+
+def test_prefill_rejects_out_of_vocab_ids_on_host():
+    g = BatchedGPT2(random_gpt2("tiny", vocab_size=700, n_positions=16), device="cpu",
+                    compute_dtype=torch.float32)
+    with pytest.raises(ValueError):
+        g.prefill([1, 2, 700], 2, 4)
+    with pytest.raises(ValueError):
+        g.prefill([-1, 2], 2, 4)
