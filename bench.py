@@ -133,9 +133,10 @@ def main():
         x = torch.randn((B, ld), generator=gen, device=dev, dtype=torch.float32).mul_(3.0)
         pool.append(x.to(tdt))
         del x
-    first = rank * B
-    payload_bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(first + s, args.payload_bytes))
-                    for s in range(B)]
+    from neuralsteganography_amd.dist import reduce_job, shard_range
+
+    mine = shard_range(B * world, world, rank)  # weak scaling: B streams per rank, disjoint payload seeds
+    payload_bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.payload_bytes)) for s in mine]
     sess = EncodeSession(ctx, payload_bits)
     stream = torch.cuda.current_stream()
 
@@ -169,16 +170,7 @@ def main():
     bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
     sess.raise_errors()
 
-    tot = torch.tensor([float(bits), float(stream_steps), elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        s = tot[:2].clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        mx = tot[2:].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        bits_all, ss_all = float(s[0]), float(s[1])
-        elapsed_max, kern_ms_max = float(mx[0]), float(mx[1])
-    else:
-        bits_all, ss_all, elapsed_max, kern_ms_max = float(bits), float(stream_steps), elapsed, kern_ms
+    bits_all, ss_all, elapsed_max, kern_ms_max = reduce_job(bits, stream_steps, elapsed, kern_ms, device=dev)
 
     from neuralsteganography_amd import _lib
 

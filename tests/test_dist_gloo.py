@@ -1,0 +1,73 @@
+"""CPU, world size 2 over gloo: stream sharding, whole-job reductions and result gathering of the
+multi-GPU path (neuralsteganography_amd/dist.py), with a deterministic CPU stand-in provider (the coder
+itself needs a GPU; what is tested here is the partitioning and the collectives around it)."""
+
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from neuralsteganography_amd.dist import shard_range
+
+
+def test_shard_range_partitions_exactly():
+    for total in (0, 1, 7, 4096, 32768, 8191):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                rg = shard_range(total, world, r)
+                seen.extend(rg)
+            assert seen == list(range(total))
+            sizes = [len(shard_range(total, world, r)) for r in range(world)]
+            assert max(sizes) - min(sizes) <= 1
+
+
+class _EchoProvider:
+    """encode_batch returns per-stream tokens derived from the bits (identity-like, deterministic)."""
+
+    def encode_batch(self, bit_lists, context, *, quality):
+        return [[len(context)] + [sum(b[i:i + 8]) for i in range(0, len(b), 8)] for b in bit_lists]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from neuralsteganography_amd import dist as nd
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bits = [[(s >> k) & 1 for k in range(16)] for s in range(11)]
+        toks = nd.encode_sharded(_EchoProvider(), bits, [1, 2, 3], quality={})
+        b, ss, el, km = nd.reduce_job(100.0 * (rank + 1), 10.0, 1.0 + rank, 0.5 * (rank + 1))
+        q.put((rank, toks, (b, ss, el, km)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world2_gloo_sharded_encode_and_reductions():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = _EchoProvider().encode_batch([[(s >> k) & 1 for k in range(16)] for s in range(11)], [1, 2, 3],
+                                          quality={})
+    for rank, toks, red in res:
+        assert toks == expect  # every rank sees all 11 streams, in stream order
+        assert red == (300.0, 20.0, 2.0, 1.0)  # bits summed, stream-steps summed, times max
