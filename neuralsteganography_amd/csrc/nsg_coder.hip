@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -341,6 +342,54 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
     c.cnt = base;
 }
 
+// exclusive prefix and total over the wave of a per-lane count n (0 <= n < 64): one ballot per bit plane
+__device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
+    excl = 0;
+    total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+        const uint64_t m = ballot(((n >> bit) & 1) != 0);
+        excl += lanes_below(m) << bit;
+        total += popc64(m) << bit;
+    }
+}
+
+// Group form of offer(): G tiles (G*W values per lane) share one reject test, one wave prefix and one
+// capacity check; passing values are written with predicated stores at lane-private positions.  If the
+// group does not fit, the per-tile path (which compacts as needed and always fits) takes over.
+template <int W, int G>
+__device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int jb, int K, int lane) {
+    constexpr int TS = WAVE * W;
+    float mx = x[0][0];
+#pragma unroll
+    for (int d = 0; d < G; ++d)
+#pragma unroll
+        for (int q = 0; q < W; ++q) mx = fmaxf(mx, x[d][q]);
+    if (!ballot(mx > c.thr)) return;
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < G; ++d)
+#pragma unroll
+        for (int q = 0; q < W; ++q) n += (x[d][q] > c.thr) ? 1 : 0;
+    int excl, total;
+    wave_excl_prefix(n, excl, total);
+    if (c.cnt + total > CAND) {
+#pragma unroll
+        for (int d = 0; d < G; ++d) offer<W>(c, x[d], jb + d * TS, K, lane);
+        return;
+    }
+    int pos = c.cnt + excl;
+#pragma unroll
+    for (int d = 0; d < G; ++d)
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            if (x[d][q] > c.thr) {
+                c.keys[pos] = make_key(x[d][q], (uint32_t)(jb + d * TS + q));
+                ++pos;
+            }
+    c.cnt += total;
+}
+
 // -inf for ids >= V (last tile only) and for banned ids (sorted; `bi`/`next_ban` advance monotonically)
 template <int W>
 __device__ __forceinline__ void mask_tile(const StepParams& p, float (&x)[W], int tile, int ntiles, int j0,
@@ -470,13 +519,24 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     // range-checked by the buffer descriptor and return zeros.
     int tile = 0;
     for (; tile + PREFETCH <= ntiles; tile += PREFETCH) {
+        float xg[PREFETCH][W];
 #pragma unroll
         for (int d = 0; d < PREFETCH; ++d) {
-            float x[W];
-            Elem<T>::unpack(buf[d], x);
-            process(x, tile + d);
+            Elem<T>::unpack(buf[d], xg[d]);
             buf[d] = rd.vec((tile + d + PREFETCH) * WAVE + lane);
         }
+        const int jb = (tile * WAVE + lane) * W;  // id of xg[d][q] = jb + d*TS + q
+        if (tile + PREFETCH == ntiles || next_ban < (tile + PREFETCH) * TS) {  // rare: tail or banned id
+#pragma unroll
+            for (int d = 0; d < PREFETCH; ++d) mask_tile<W>(p, xg[d], tile + d, ntiles, jb + d * TS, bi, next_ban);
+        }
+        float a = 0.0f;
+#pragma unroll
+        for (int d = 0; d < PREFETCH; ++d)
+#pragma unroll
+            for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((xg[d][q] - r) * c32);
+        acc64 += (double)a;
+        offer_group<W, PREFETCH>(cand, xg, jb, K, lane);
     }
 #pragma unroll
     for (int d = 0; d < PREFETCH; ++d) {
@@ -575,7 +635,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         const double u24 = 5.9604644775390625e-08;  // 2^-24
         const double eb = 9.5367431640625e-07         // v_exp_f32 error (2^-20, generous)
                           + 3.0 * u24 * 0.6931471805599453 * (60.0 + fabs(t_m))  // argument rounding
-                          + (double)(W + 1) * u24                                   // fp32 partials
+                          + (double)(PREFETCH * W + 1) * u24                        // fp32 partials
                           + 1.0e-13;
         const double B2 = 2.0 * eb + 1.0e-12;
         // reciprocals with an extra 1e-15 margin stand in for the per-element divisions
@@ -850,7 +910,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.2 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.3 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -945,10 +1005,14 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     // speculative candidate threshold: the spec_j-th largest of a 1024-id stratified sample, chosen so that
     // about 3.2*K ids of the row pass it (a guess verified per row; a miss costs one extra row read)
     p.spec_j = 0;
-    if (ctx->vocab >= 2048) {
-        const double j = 3.2 * (double)K * 1024.0 / (double)nvalid;
+    static const double spec_factor = [] {  // tuning override (tools/): expected passes = factor * K
+        const char* e = getenv("NSG_SPEC_FACTOR");
+        return e ? atof(e) : 3.2;
+    }();
+    if (ctx->vocab >= 2048 && spec_factor > 0.0) {
+        const double j = spec_factor * (double)K * 1024.0 / (double)nvalid;
         int sj = (int)j + 1;
-        if (sj < 16) sj = 16;
+        if (sj < 4) sj = 4;
         if (sj < 256) p.spec_j = sj;
     }
     p.state = d_state;
