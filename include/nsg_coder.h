@@ -83,13 +83,15 @@ typedef struct ns_ctx ns_ctx;
 
 /* Create a context on `device` for logits rows of `vocab` entries of `logits_dtype` (NS_DTYPE_*),
  * at most `max_batch` streams per call, interval precision `precision` (1..60 bits) and top-k up to
- * `max_k` (must be <= ns_max_topk(logits_dtype)).  Returns NULL on failure (see ns_last_error(NULL)). */
+ * `max_k`.  max_k <= ns_max_topk(dtype) uses the single-pass kernel only; a larger max_k also allocates
+ * the wide path (stats pass, collect, segmented radix sort, workgroup CDF; 16 B x max_batch x vocab of
+ * scratch, vocab < 131072).  Returns NULL on failure (see ns_last_error(NULL)). */
 ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision, int logits_dtype);
 void ns_destroy(ns_ctx* ctx);
 const char* ns_last_error(const ns_ctx* ctx);
 const char* ns_version(void);
 
-/* Largest topk the single-pass kernel supports for a logits dtype. */
+/* Largest topk the single-pass kernel handles for a logits dtype (larger topk takes the wide path). */
 int ns_max_topk(int logits_dtype);
 
 /* Reset B stream states to [0, 2^precision), bit_pos 0. */

@@ -99,12 +99,9 @@ class CoderContext:
         self.device = torch.cuda.current_device() if device is None else int(device)
         self.max_batch = int(max_batch)
         L = _lib.lib()
-        kmax = L.ns_max_topk(params.dtype_code)
         vocab_valid = params.vocab - len({b for b in params.banned_ids() if 0 <= b < params.vocab})
         self.K = min(params.topk, vocab_valid)
-        if self.K > kmax:
-            raise ConfigurationError(
-                f"topk={params.topk} exceeds the single-pass HIP kernel limit {kmax} for {params.dtype} logits")
+        self.wide = self.K > L.ns_max_topk(params.dtype_code)  # large top-k: multi-kernel wide path
         handle = L.ns_create(self.device, self.max_batch, params.vocab, max(1, self.K), params.precision,
                              params.dtype_code)
         if not handle:

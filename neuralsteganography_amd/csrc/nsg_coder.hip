@@ -32,196 +32,11 @@
 
 #pragma clang fp contract(off)
 
+#include "nsg_common.h"
+#include "nsg_host.h"
+#include "nsg_host.h"
+
 namespace nsg {
-
-#ifndef NSG_WPB
-#define NSG_WPB 4
-#endif
-#ifndef NSG_CAND
-#define NSG_CAND 1024
-#endif
-#ifndef NSG_PREFETCH
-#define NSG_PREFETCH 8
-#endif
-#ifndef NSG_MIN_WAVES_PER_EU
-#define NSG_MIN_WAVES_PER_EU 4
-#endif
-
-constexpr int WAVE = 64;
-#define NS_COUNTER_SHARDS 256
-constexpr int WPB = NSG_WPB;            // waves (streams) per workgroup
-constexpr int CAND = NSG_CAND;          // candidate keys per wave (8 B each, LDS)
-constexpr int PREFETCH = NSG_PREFETCH;  // tiles in flight per wave
-
-// ------------------------------------------------------------------------------------------------
-// canonical float64 exp -- identical operation sequence to or_exp_canon (oracle/nsg_oracle.c)
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double exp_canon(double d) {
-    if (!(d >= -700.0)) return 0.0;
-    const double n = __builtin_rint(d * 1.44269504088896338700e+00);
-    double r = __builtin_fma(-n, 6.93147180369123816490e-01, d);
-    r = __builtin_fma(-n, 1.90821492927058770002e-10, r);
-    double p = 1.60590438368216145994e-10;
-    p = __builtin_fma(p, r, 2.08767569878680989792e-09);
-    p = __builtin_fma(p, r, 2.50521083854417187751e-08);
-    p = __builtin_fma(p, r, 2.75573192239858906526e-07);
-    p = __builtin_fma(p, r, 2.75573192239858906526e-06);
-    p = __builtin_fma(p, r, 2.48015873015873015873e-05);
-    p = __builtin_fma(p, r, 1.98412698412698412698e-04);
-    p = __builtin_fma(p, r, 1.38888888888888888889e-03);
-    p = __builtin_fma(p, r, 8.33333333333333333333e-03);
-    p = __builtin_fma(p, r, 4.16666666666666666667e-02);
-    p = __builtin_fma(p, r, 1.66666666666666666667e-01);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    return __builtin_ldexp(p, (int)n);
-}
-
-// ------------------------------------------------------------------------------------------------
-// keys: (value desc, id asc) as one descending uint64
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ord32(float x) {
-    x = x + 0.0f;  // -0 -> +0
-    const uint32_t u = __float_as_uint(x);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float unord32(uint32_t o) {
-    const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
-    return __uint_as_float(u);
-}
-__device__ __forceinline__ uint64_t make_key(float x, uint32_t j) {
-    return ((uint64_t)ord32(x) << 32) | (uint64_t)(0xFFFFFFFFu - j);
-}
-__device__ __forceinline__ uint32_t key_id(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
-__device__ __forceinline__ float key_val(uint64_t k) { return unord32((uint32_t)(k >> 32)); }
-
-// ------------------------------------------------------------------------------------------------
-// wave helpers
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
-__device__ __forceinline__ void lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-__device__ __forceinline__ double wave_sum_butterfly(double v) {
-    // canonical xor butterfly 32,16,8,4,2,1 (commutative per pair => every lane ends identical)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
-    return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-    return v;
-}
-__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        const int64_t y = __shfl_up(v, off);
-        if (lane >= off) v += y;
-    }
-    return v;
-}
-
-// ------------------------------------------------------------------------------------------------
-// logit loads
-// ------------------------------------------------------------------------------------------------
-template <typename T>
-struct Elem;
-template <>
-struct Elem<float> {
-    static constexpr int W = 4;
-    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[4]) {
-        x[0] = __uint_as_float(v.x);
-        x[1] = __uint_as_float(v.y);
-        x[2] = __uint_as_float(v.z);
-        x[3] = __uint_as_float(v.w);
-    }
-    __device__ static __forceinline__ float load1(const void* row, int j) { return ((const float*)row)[j]; }
-};
-template <>
-struct Elem<_Float16> {
-    static constexpr int W = 8;
-    __device__ static __forceinline__ float h2f(uint32_t bits16) {
-        const uint16_t b = (uint16_t)bits16;
-        _Float16 h;
-        __builtin_memcpy(&h, &b, 2);
-        return (float)h;
-    }
-    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[8]) {
-        x[0] = h2f(v.x & 0xFFFFu);
-        x[1] = h2f(v.x >> 16);
-        x[2] = h2f(v.y & 0xFFFFu);
-        x[3] = h2f(v.y >> 16);
-        x[4] = h2f(v.z & 0xFFFFu);
-        x[5] = h2f(v.z >> 16);
-        x[6] = h2f(v.w & 0xFFFFu);
-        x[7] = h2f(v.w >> 16);
-    }
-    __device__ static __forceinline__ float load1(const void* row, int j) {
-        return h2f(((const uint16_t*)row)[j]);
-    }
-};
-
-// ------------------------------------------------------------------------------------------------
-// step parameters (kernel argument, by value)
-// ------------------------------------------------------------------------------------------------
-struct StepParams {
-    const void* logits;
-    int64_t ld;
-    int B, V, P, topk, K;  // K = min(topk, #valid ids)
-    double inv_temp;
-    float c32;  // (float)(inv_temp * log2(e))
-    int nbanned;
-    int banned[NS_MAX_BANNED];  // sorted ascending, unique, in [0, V)
-    int spec_j;  // speculative threshold rank in the 1024-id sample (0: no sample)
-    uint32_t flags;
-    // encode
-    const uint8_t* payload;
-    int64_t payload_stride;
-    const int64_t* nbits;
-    int32_t* out_token;
-    int32_t* hist;
-    int64_t hist_stride;
-    // decode
-    const int32_t* in_token;
-    const uint8_t* is_last;
-    const uint8_t* active;
-    uint8_t* out_bits;
-    int64_t out_stride;
-    // common
-    ns_stream_state* state;
-    ns_step_trace* trace;
-    unsigned long long* counters;
-};
-
-__device__ __forceinline__ bool is_banned(const StepParams& p, int j) {
-    bool b = false;
-#pragma unroll
-    for (int i = 0; i < NS_MAX_BANNED; ++i) b |= (i < p.nbanned) && (p.banned[i] == j);
-    return b;
-}
-
-// exact canonical row sum (oracle or_row_sum): id j -> lane (j>>2)&63, per-lane increasing, butterfly
-template <typename T>
-__device__ __forceinline__ double exact_row_sum(const StepParams& p, const void* row, double m, int lane) {
-    double acc = 0.0;
-    const int ngroups = (p.V + 3) >> 2;
-    for (int g = lane; g < ngroups; g += WAVE) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = 4 * g + q;
-            if (j < p.V && !is_banned(p, j)) {
-                const float x = Elem<T>::load1(row, j) + 0.0f;
-                acc += exp_canon(((double)x - m) * p.inv_temp);
-            }
-        }
-    }
-    return wave_sum_butterfly(acc);
-}
 
 // Keep exactly the top-K keys of keys[0..cnt) (cnt >= K).  Bisection on the value word, then on the id
 // word among ties; counts by ballot+popcount.  Returns the K-th key.
@@ -281,24 +96,6 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, int cnt, int K, in
 }
 
 // buffer-resource row reader: one SRD per wave (uniform), range-checked 16-byte loads (0 beyond the row)
-__device__ __forceinline__ const void* uniform_ptr(const void* ptr) {
-    const uint64_t a = (uint64_t)ptr;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return (const void*)(((uint64_t)hi << 32) | lo);
-}
-
-struct RowReader {
-    __amdgpu_buffer_rsrc_t rs;
-    __device__ __forceinline__ RowReader(const void* base, uint32_t bytes)
-        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), (short)0,
-                                               (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000)) {}
-    __device__ __forceinline__ uint4 vec(int v) const {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, 0);
-        return make_uint4(r[0], r[1], r[2], r[3]);
-    }
-};
-
 // Candidate buffer of one wave: keys of every element > thr seen so far (a superset of the running top-K).
 struct Cand {
     uint64_t* keys;
@@ -853,16 +650,6 @@ __global__ void init_state_kernel(ns_stream_state* st, int B, int P) {
 // ================================================================================================
 // C ABI
 // ================================================================================================
-struct ns_ctx {
-    int device;
-    int max_batch;
-    int vocab;
-    int max_k;
-    int precision;
-    int dtype;
-    unsigned long long* d_counters;
-    std::string err;
-};
 
 static thread_local std::string g_err;
 
@@ -910,7 +697,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.3 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.4 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -925,8 +712,8 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
         fail(nullptr, NS_ERR_CONFIG, "ns_create: invalid argument");
         return nullptr;
     }
-    if (max_k > ns_max_topk(logits_dtype)) {
-        fail(nullptr, NS_ERR_UNSUPPORTED, "ns_create: max_k exceeds the single-pass kernel limit");
+    if (max_k > ns_max_topk(logits_dtype) && vocab > 0x1FFFF) {
+        fail(nullptr, NS_ERR_UNSUPPORTED, "ns_create: the wide (large top-k) path supports vocab < 131072");
         return nullptr;
     }
     if (hipSetDevice(device) != hipSuccess) {
@@ -941,9 +728,17 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->precision = precision;
     ctx->dtype = logits_dtype;
     ctx->d_counters = nullptr;
+    ctx->wide = NsgWide();
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
+        delete ctx;
+        return nullptr;
+    }
+    if (max_k > ns_max_topk(logits_dtype) && nsg_wide_alloc(ctx) != NS_OK) {
+        fail(nullptr, NS_ERR_HIP, "ns_create: allocation of the wide-path scratch failed");
+        nsg_wide_free(ctx);
+        (void)hipFree(ctx->d_counters);
         delete ctx;
         return nullptr;
     }
@@ -953,6 +748,7 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
 void ns_destroy(ns_ctx* ctx) {
     if (!ctx) return;
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    nsg_wide_free(ctx);
     delete ctx;
 }
 
@@ -987,8 +783,9 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     const int nvalid = ctx->vocab - nb;
     if (nvalid < 2) return fail(ctx, NS_ERR_CONFIG, "fewer than two valid token ids");
     const int K = std::min(topk, nvalid);
-    if (K > ns_max_topk(ctx->dtype))
-        return fail(ctx, NS_ERR_UNSUPPORTED, "topk beyond the single-pass kernel limit (ns_max_topk)");
+    if (K > ns_max_topk(ctx->dtype) && !ctx->wide.keys_in)
+        return fail(ctx, NS_ERR_UNSUPPORTED,
+                    "topk beyond the single-pass limit (ns_max_topk): create the context with max_k >= topk");
     memset(&p, 0, sizeof p);
     p.logits = d_logits;
     p.ld = ld;
@@ -1038,7 +835,9 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
     p.out_token = d_out_token;
     p.hist = d_token_hist;
     p.hist_stride = d_token_hist ? hist_stride : 0;
-    if (!launch<false>(ctx, p, (hipStream_t)hip_stream)) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
+    const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, false, (hipStream_t)hip_stream)
+                                                  : launch<false>(ctx, p, (hipStream_t)hip_stream);
+    if (!ok) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
     return NS_OK;
 }
 
@@ -1056,7 +855,9 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
     p.active = d_active;
     p.out_bits = d_out_bits;
     p.out_stride = out_stride;
-    if (!launch<true>(ctx, p, (hipStream_t)hip_stream)) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
+    const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, true, (hipStream_t)hip_stream)
+                                                  : launch<true>(ctx, p, (hipStream_t)hip_stream);
+    if (!ok) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
     return NS_OK;
 }
 

@@ -1,0 +1,242 @@
+// nsg_common.h -- device helpers shared by the single-pass coder kernel (nsg_coder.hip) and the
+// wide (large top-k) path (nsg_wide.hip).  Canonical arithmetic here must stay bit-identical to
+// oracle/nsg_oracle.c.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nsg_coder.h"
+
+#pragma clang fp contract(off)
+
+namespace nsg {
+
+#ifndef NSG_WPB
+#define NSG_WPB 4
+#endif
+#ifndef NSG_CAND
+#define NSG_CAND 1024
+#endif
+#ifndef NSG_PREFETCH
+#define NSG_PREFETCH 8
+#endif
+#ifndef NSG_MIN_WAVES_PER_EU
+#define NSG_MIN_WAVES_PER_EU 4
+#endif
+
+constexpr int WAVE = 64;
+#define NS_COUNTER_SHARDS 256
+constexpr int WPB = NSG_WPB;            // waves (streams) per workgroup
+constexpr int CAND = NSG_CAND;          // candidate keys per wave (8 B each, LDS)
+constexpr int PREFETCH = NSG_PREFETCH;  // tiles in flight per wave
+
+// ------------------------------------------------------------------------------------------------
+// canonical float64 exp -- identical operation sequence to or_exp_canon (oracle/nsg_oracle.c)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double exp_canon(double d) {
+    if (!(d >= -700.0)) return 0.0;
+    const double n = __builtin_rint(d * 1.44269504088896338700e+00);
+    double r = __builtin_fma(-n, 6.93147180369123816490e-01, d);
+    r = __builtin_fma(-n, 1.90821492927058770002e-10, r);
+    double p = 1.60590438368216145994e-10;
+    p = __builtin_fma(p, r, 2.08767569878680989792e-09);
+    p = __builtin_fma(p, r, 2.50521083854417187751e-08);
+    p = __builtin_fma(p, r, 2.75573192239858906526e-07);
+    p = __builtin_fma(p, r, 2.75573192239858906526e-06);
+    p = __builtin_fma(p, r, 2.48015873015873015873e-05);
+    p = __builtin_fma(p, r, 1.98412698412698412698e-04);
+    p = __builtin_fma(p, r, 1.38888888888888888889e-03);
+    p = __builtin_fma(p, r, 8.33333333333333333333e-03);
+    p = __builtin_fma(p, r, 4.16666666666666666667e-02);
+    p = __builtin_fma(p, r, 1.66666666666666666667e-01);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
+
+// ------------------------------------------------------------------------------------------------
+// keys: (value desc, id asc) as one descending uint64
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord32(float x) {
+    x = x + 0.0f;  // -0 -> +0
+    const uint32_t u = __float_as_uint(x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord32(uint32_t o) {
+    const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    return __uint_as_float(u);
+}
+__device__ __forceinline__ uint64_t make_key(float x, uint32_t j) {
+    return ((uint64_t)ord32(x) << 32) | (uint64_t)(0xFFFFFFFFu - j);
+}
+__device__ __forceinline__ uint32_t key_id(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ float key_val(uint64_t k) { return unord32((uint32_t)(k >> 32)); }
+
+// ------------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ void lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ double wave_sum_butterfly(double v) {
+    // canonical xor butterfly 32,16,8,4,2,1 (commutative per pair => every lane ends identical)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const int64_t y = __shfl_up(v, off);
+        if (lane >= off) v += y;
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// logit loads
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct Elem;
+template <>
+struct Elem<float> {
+    static constexpr int W = 4;
+    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[4]) {
+        x[0] = __uint_as_float(v.x);
+        x[1] = __uint_as_float(v.y);
+        x[2] = __uint_as_float(v.z);
+        x[3] = __uint_as_float(v.w);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int j) { return ((const float*)row)[j]; }
+};
+template <>
+struct Elem<_Float16> {
+    static constexpr int W = 8;
+    __device__ static __forceinline__ float h2f(uint32_t bits16) {
+        const uint16_t b = (uint16_t)bits16;
+        _Float16 h;
+        __builtin_memcpy(&h, &b, 2);
+        return (float)h;
+    }
+    __device__ static __forceinline__ void unpack(const uint4& v, float (&x)[8]) {
+        x[0] = h2f(v.x & 0xFFFFu);
+        x[1] = h2f(v.x >> 16);
+        x[2] = h2f(v.y & 0xFFFFu);
+        x[3] = h2f(v.y >> 16);
+        x[4] = h2f(v.z & 0xFFFFu);
+        x[5] = h2f(v.z >> 16);
+        x[6] = h2f(v.w & 0xFFFFu);
+        x[7] = h2f(v.w >> 16);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int j) {
+        return h2f(((const uint16_t*)row)[j]);
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// step parameters (kernel argument, by value)
+// ------------------------------------------------------------------------------------------------
+struct StepParams {
+    const void* logits;
+    int64_t ld;
+    int B, V, P, topk, K;  // K = min(topk, #valid ids)
+    double inv_temp;
+    float c32;  // (float)(inv_temp * log2(e))
+    int nbanned;
+    int banned[NS_MAX_BANNED];  // sorted ascending, unique, in [0, V)
+    int spec_j;  // speculative threshold rank in the 1024-id sample (0: no sample)
+    uint32_t flags;
+    // encode
+    const uint8_t* payload;
+    int64_t payload_stride;
+    const int64_t* nbits;
+    int32_t* out_token;
+    int32_t* hist;
+    int64_t hist_stride;
+    // decode
+    const int32_t* in_token;
+    const uint8_t* is_last;
+    const uint8_t* active;
+    uint8_t* out_bits;
+    int64_t out_stride;
+    // common
+    ns_stream_state* state;
+    ns_step_trace* trace;
+    unsigned long long* counters;
+};
+
+__device__ __forceinline__ bool is_banned(const StepParams& p, int j) {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NS_MAX_BANNED; ++i) b |= (i < p.nbanned) && (p.banned[i] == j);
+    return b;
+}
+
+// exact canonical row sum (oracle or_row_sum): id j -> lane (j>>2)&63, per-lane increasing, butterfly
+template <typename T>
+__device__ __forceinline__ double exact_row_sum(const StepParams& p, const void* row, double m, int lane) {
+    double acc = 0.0;
+    const int ngroups = (p.V + 3) >> 2;
+    for (int g = lane; g < ngroups; g += WAVE) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 4 * g + q;
+            if (j < p.V && !is_banned(p, j)) {
+                const float x = Elem<T>::load1(row, j) + 0.0f;
+                acc += exp_canon(((double)x - m) * p.inv_temp);
+            }
+        }
+    }
+    return wave_sum_butterfly(acc);
+}
+
+__device__ __forceinline__ const void* uniform_ptr(const void* ptr) {
+    const uint64_t a = (uint64_t)ptr;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (const void*)(((uint64_t)hi << 32) | lo);
+}
+
+struct RowReader {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ RowReader(const void* base, uint32_t bytes)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), (short)0,
+                                               (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000)) {}
+    __device__ __forceinline__ uint4 vec(int v) const {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, 0);
+        return make_uint4(r[0], r[1], r[2], r[3]);
+    }
+};
+
+// Proven interval of the canonical float64 row sum S from the fast estimate S_r = sum 2^((x-r)*c32)
+// accumulated in fp32 groups of at most `fp32_terms` terms.  Returns false when the
+// bound is unusable (overflow/underflow of the estimate, reference too far from the max).
+__device__ __forceinline__ bool fast_sum_interval(double S_r, float r, double m, float c32, double inv_temp,
+                                                  int fp32_terms, double& Sf, double& S_lo, double& S_hi) {
+    const double t_m = (m - (double)r) * (double)c32;
+    if (!(S_r > 0.0 && S_r < 1.0e300) || !(t_m <= 100.0 && t_m >= -60.0)) return false;
+    const double f = exp_canon(((double)r - m) * inv_temp);
+    Sf = S_r * f;
+    const double u24 = 5.9604644775390625e-08;  // 2^-24
+    const double eb = 9.5367431640625e-07         // v_exp_f32 error (2^-20, generous)
+                      + 3.0 * u24 * 0.6931471805599453 * (60.0 + fabs(t_m))  // argument rounding
+                      + (double)(fp32_terms + 1) * u24                          // fp32 partials
+                      + 1.0e-13;
+    const double B2 = 2.0 * eb + 1.0e-12;
+    S_lo = Sf * (1.0 - B2);
+    S_hi = Sf * (1.0 + B2);
+    return true;
+}
+
+}  // namespace nsg

@@ -1,0 +1,55 @@
+// nsg_host.h -- host-side context shared by the single-pass path (nsg_coder.hip) and the wide path
+// (nsg_wide.hip).  Not part of the public ABI (include/nsg_coder.h only sees an opaque ns_ctx).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "nsg_common.h"
+
+namespace nsg {
+
+// per-stream statistics of the wide path's first pass
+struct WideStat {
+    float m;          // row max (valid ids)
+    float m2;         // second largest value (>= 2 ids are always collected)
+    float r;          // reference of the fast sum
+    uint32_t active;  // 0: stream done/inactive this step
+    double S_lo;      // proven interval of the canonical float64 row sum
+    double S_hi;
+    double S_fast;
+    uint32_t exact;   // 1: the fast bound is unusable, the CDF kernel computes the exact sum
+    uint32_t pad;
+};
+
+}  // namespace nsg
+
+struct NsgWide {
+    int cap = 0;                    // keys per stream segment (= vocab)
+    uint64_t* keys_in = nullptr;    // [max_batch * cap]
+    uint64_t* keys_out = nullptr;   // [max_batch * cap]
+    unsigned int* count = nullptr;  // [max_batch] collected ids per stream
+    unsigned int* begin = nullptr;  // [max_batch] segment offsets for the sort
+    unsigned int* end = nullptr;    // [max_batch]
+    nsg::WideStat* stat = nullptr;  // [max_batch]
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+};
+
+struct ns_ctx {
+    int device;
+    int max_batch;
+    int vocab;
+    int max_k;
+    int precision;
+    int dtype;
+    unsigned long long* d_counters;
+    NsgWide wide;
+    std::string err;
+};
+
+// wide (top-k beyond the single-pass limit) path, nsg_wide.hip
+int nsg_wide_alloc(ns_ctx* ctx);  // NS_OK or NS_ERR_HIP
+void nsg_wide_free(ns_ctx* ctx);
+bool nsg_wide_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s);

@@ -1,0 +1,505 @@
+// nsg_wide.hip -- the coder step for top-k beyond the single-pass kernel's LDS candidate buffer
+// (e.g. the api default topk 50,000 at precision 16, or the message->bits mode, precision 40 / topk 60,000,
+// code_base/run_single.py:52-54).  Same canonical arithmetic as the single-pass kernel and the oracle.
+//
+//   1. wide_stats_kernel   (wave per stream)  : one streaming pass -> row max, second max, fast-sum interval
+//   2. wide_collect_kernel (blocks per chunk) : every id that can clear the 1/R cutoff, plus the top two,
+//                                               written as 49-bit (value desc, id asc) keys to a segment
+//   3. rocprim::segmented_radix_sort_keys_desc : per-stream descending sort of the collected keys
+//   4. wide_cdf_kernel     (1024 threads/stream): cutoff, canonical sums, rint, int64 scan, overfill,
+//                                               selection, interval update
+// An id left out by step 2 has e_i < S_lo/R <= S/R, i.e. p_i < 1/R for certain, so the first rank below the
+// cutoff lies inside the collected prefix or right after it.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include "nsg_common.h"
+#include "nsg_host.h"
+
+#pragma clang fp contract(off)
+
+namespace nsg {
+
+constexpr int WIDE_THREADS = 1024;
+constexpr int WIDE_ROUND = 8192;  // doubles staged in LDS per round (64 KiB)
+constexpr int COLLECT_CHUNK = 4096;
+
+// 49-bit wide keys: ord(value) << 17 | (0x1FFFF - id); ids < 2^17
+__device__ __forceinline__ uint64_t wkey(float x, uint32_t j) {
+    return ((uint64_t)ord32(x) << 17) | (uint64_t)(0x1FFFFu - j);
+}
+__device__ __forceinline__ uint32_t wkey_id(uint64_t k) { return 0x1FFFFu - (uint32_t)(k & 0x1FFFFu); }
+__device__ __forceinline__ float wkey_val(uint64_t k) { return unord32((uint32_t)(k >> 17)); }
+
+// ------------------------------------------------------------------------------------------ pass 1
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, WideStat* ws, unsigned int* count) {
+    constexpr int W = Elem<T>::W;
+    constexpr int TS = WAVE * W;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + (int)(threadIdx.x / WAVE));
+    if (b >= p.B) return;
+    const ns_stream_state st = p.state[b];
+    bool active = !(st.flags & NS_ST_DONE);
+    if (!DECODE && active && st.bit_pos >= p.nbits[b]) {
+        if (lane == 0) p.state[b].flags = st.flags | NS_ST_DONE;
+        active = false;
+    }
+    if (DECODE && p.active && !p.active[b]) active = false;
+    if (!active) {
+        if (lane == 0) {
+            ws[b].active = 0;
+            count[b] = 0;
+        }
+        return;
+    }
+    const int V = p.V;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int ntiles = (V + TS - 1) / TS;
+    float r = 0.0f, m1 = -__builtin_inff(), m2 = -__builtin_inff();
+    double acc64 = 0.0;
+    int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+    for (int tile = 0; tile < ntiles; ++tile) {
+        float x[W];
+        Elem<T>::unpack(rd.vec(tile * WAVE + lane), x);
+        const int j0 = (tile * WAVE + lane) * W;
+        if (tile == ntiles - 1) {
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (j0 + q >= V) x[q] = -__builtin_inff();
+        }
+        while (next_ban < (tile + 1) * TS) {
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (j0 + q == next_ban) x[q] = -__builtin_inff();
+            ++bi;
+            next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+        }
+        if (tile == 0) {
+            float mx = x[0];
+#pragma unroll
+            for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+            r = wave_max(mx);
+            if (r == -__builtin_inff()) r = 0.0f;
+        }
+        float a = 0.0f;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            a += __builtin_amdgcn_exp2f((x[q] - r) * p.c32);
+            m2 = fmaxf(m2, fminf(m1, x[q]));
+            m1 = fmaxf(m1, x[q]);
+        }
+        acc64 += (double)a;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
+        m2 = fmaxf(fminf(m1, o1), fmaxf(m2, o2));
+        m1 = fmaxf(m1, o1);
+    }
+    const double S_r = wave_sum_butterfly(acc64);
+    double Sf = 0.0, S_lo = 0.0, S_hi = 0.0;
+    const bool ok = fast_sum_interval(S_r, r, (double)(m1 + 0.0f), p.c32, p.inv_temp, W, Sf, S_lo, S_hi);
+    if (lane == 0) {
+        WideStat w;
+        w.m = m1;
+        w.m2 = m2;
+        w.r = r;
+        w.active = 1;
+        w.S_lo = S_lo;
+        w.S_hi = S_hi;
+        w.S_fast = Sf;
+        w.exact = (ok && !(p.flags & NS_STEP_FORCE_EXACT_SUM)) ? 0u : 1u;
+        w.pad = 0;
+        ws[b] = w;
+        count[b] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------ pass 2
+template <typename T>
+__global__ __launch_bounds__(256) void wide_collect_kernel(StepParams p, const WideStat* ws, uint64_t* keys,
+                                                           unsigned int* count, int cap) {
+    constexpr int W = Elem<T>::W;
+    constexpr int PER_THREAD = COLLECT_CHUNK / 256;  // ids per thread
+    const int b = blockIdx.y;
+    const WideStat w = ws[b];
+    if (!w.active) return;
+    const int V = p.V;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const ns_stream_state st = p.state[b];
+    const double thr = 1.0 / (double)(st.hi - st.lo);
+    float xt;
+    if (w.exact) {
+        xt = -__builtin_inff();  // collect every valid id
+    } else {
+        // e(x) >= S_lo/R  <=>  x >= m + temp * ln(S_lo/R); widened generously (extra ids are harmless)
+        const double temp = 1.0 / p.inv_temp;
+        const double L = log(w.S_lo * thr);
+        const double t = (double)w.m + temp * L;
+        xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + fabs(temp * L)));
+    }
+    xt = fminf(xt, w.m2);  // at least the top two ids (k >= 2)
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int base_id = blockIdx.x * COLLECT_CHUNK;
+#pragma unroll
+    for (int i = 0; i < PER_THREAD / W; ++i) {
+        const int j0 = base_id + (i * 256 + (int)threadIdx.x) * W;
+        float x[W];
+        Elem<T>::unpack(rd.vec(j0 / W), x);
+        uint64_t msk[W];
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            const int j = j0 + q;
+            const bool take = j < V && !is_banned(p, j) && x[q] >= xt;
+            msk[q] = ballot(take);
+            tot += popc64(msk[q]);
+        }
+        if (tot == 0) continue;
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(&count[b], (unsigned int)tot);
+        base = __shfl(base, 0);
+        int off = 0;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            const int j = j0 + q;
+            if ((msk[q] >> lane) & 1ull)
+                keys[(int64_t)b * cap + base + off + lanes_below(msk[q])] = wkey(x[q], (uint32_t)j);
+            off += popc64(msk[q]);
+        }
+    }
+}
+
+__global__ void wide_offsets_kernel(int B, int cap, const WideStat* ws, const unsigned int* count,
+                                    unsigned int* begin, unsigned int* end) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) {
+        begin[b] = (unsigned int)(b * cap);
+        end[b] = (unsigned int)(b * cap) + (ws[b].active ? count[b] : 0u);
+    }
+}
+
+// ------------------------------------------------------------------------------------------ pass 4
+// block helpers (1024 threads = 16 waves)
+__device__ __forceinline__ int block_min_int(int v, int* sm) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+    __syncthreads();
+    if (lane == 0) sm[w] = v;
+    __syncthreads();
+    int r = sm[0];
+    for (int i = 1; i < WIDE_THREADS / 64; ++i) r = min(r, sm[i]);
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sm, int64_t& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t inc = wave_incl_scan(v, lane);
+    __syncthreads();
+    if (lane == 63) sm[w] = inc;
+    __syncthreads();
+    int64_t before = 0, all = 0;
+    for (int i = 0; i < WIDE_THREADS / 64; ++i) {
+        if (i < w) before += sm[i];
+        all += sm[i];
+    }
+    __syncthreads();
+    total = all;
+    return before + inc - v;
+}
+
+// canonical butterfly over 64 lane partials held in sm64[0..63] (thread l < 64 owns lane l)
+__device__ __forceinline__ double block_canonical_butterfly(double* sm64) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        double t = 0.0;
+        if (threadIdx.x < 64) t = sm64[threadIdx.x] + sm64[threadIdx.x ^ off];
+        __syncthreads();
+        if (threadIdx.x < 64) sm64[threadIdx.x] = t;
+        __syncthreads();
+    }
+    return sm64[0];
+}
+
+template <typename T>
+__device__ double block_exact_row_sum(const StepParams& p, const char* rowc, double m, double* ebuf, double* sm64) {
+    // canonical order: id j -> lane (j>>2)&63, per-lane increasing; exps computed in parallel per round
+    double acc = 0.0;
+    for (int base = 0; base < p.V; base += WIDE_ROUND) {
+        for (int i = threadIdx.x; i < WIDE_ROUND; i += WIDE_THREADS) {
+            const int j = base + i;
+            double e = 0.0;
+            if (j < p.V && !is_banned(p, j)) e = exp_canon(((double)(Elem<T>::load1(rowc, j) + 0.0f) - m) * p.inv_temp);
+            ebuf[i] = e;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            // groups of this round in increasing order: g = base/4 + g_local, lane = g & 63
+            const int g0 = base / 4;
+            for (int gl = ((int)threadIdx.x - g0 % 64 + 64) % 64; gl < WIDE_ROUND / 4; gl += 64) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc += ebuf[4 * gl + q];
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 64) sm64[threadIdx.x] = acc;
+    __syncthreads();
+    return block_canonical_butterfly(sm64);
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, const WideStat* ws,
+                                                                const uint64_t* keys_sorted,
+                                                                const unsigned int* count, int cap) {
+    __shared__ double ebuf[WIDE_ROUND];
+    __shared__ double sm64[64];
+    __shared__ int smi[16];
+    __shared__ int64_t sml[16];
+    __shared__ int64_t cum_at[4];  // [0] cum(kp-1), [1] cum(sel-1), [2] cum(sel)
+    __shared__ uint64_t sel_key;
+    const int b = blockIdx.x;
+    const WideStat w = ws[b];
+    if (!w.active) return;
+    const int tid = threadIdx.x;
+    const ns_stream_state st = p.state[b];
+    const uint64_t* sk = keys_sorted + (int64_t)b * cap;
+    const int nC = (int)count[b];
+    const int Kc = min(nC, p.K);
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const double m = (double)wkey_val(sk[0]);
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R;
+    const double thr = 1.0 / Rd;
+    auto e_of = [&](int i) -> double { return exp_canon(((double)wkey_val(sk[i]) - m) * p.inv_temp); };
+
+    // ---- 1. cutoff k0 = first rank with e_i/S < thr (ranks >= Kc are below for certain)
+    bool exact = w.exact != 0;
+    int k0 = Kc;
+    double S_used = w.S_fast;
+    if (!exact) {
+        const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15));
+        const double inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
+        int fb = Kc, fa = Kc;
+        for (int i = tid; i < Kc; i += WIDE_THREADS) {
+            const double e = e_of(i);
+            const bool below = e * inv_lo < thr;
+            const bool above = e * inv_hi >= thr;
+            if (below && i < fb) fb = i;
+            if (!below && !above && i < fa) fa = i;
+        }
+        fb = block_min_int(fb, smi);
+        fa = block_min_int(fa, smi);
+        if (fa < fb)
+            exact = true;
+        else
+            k0 = fb;
+    }
+    if (exact) {
+        const double S = block_exact_row_sum<T>(p, rowc, m, ebuf, sm64);
+        S_used = S;
+        int fb = Kc;
+        for (int i = tid; i < Kc; i += WIDE_THREADS)
+            if (e_of(i) / S < thr && i < fb) fb = i;
+        k0 = block_min_int(fb, smi);
+    }
+    int k = k0 < 2 ? 2 : k0;
+    if (k > p.topk) k = p.topk;
+
+    // ---- 2. E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
+    double acc = 0.0;
+    for (int base = 0; base < k; base += WIDE_ROUND) {
+        for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < k) ? e_of(base + i) : 0.0;
+        __syncthreads();
+        if (tid < 64)
+            for (int i = tid; i < WIDE_ROUND && base + i < k; i += 64) acc += ebuf[i];
+        __syncthreads();
+    }
+    if (tid < 64) sm64[tid] = acc;
+    __syncthreads();
+    const double E = block_canonical_butterfly(sm64);
+
+    // ---- 3. q_i = rint(e_i/E*R), inclusive prefix over contiguous rank chunks, overfill trim
+    const int cs = (k + WIDE_THREADS - 1) / WIDE_THREADS;
+    const int i0 = min(k, tid * cs), i1 = min(k, i0 + cs);
+    auto q_of = [&](int i) -> int64_t { return (int64_t)__builtin_rint((e_of(i) / E) * Rd); };
+    int64_t local = 0;
+    for (int i = i0; i < i1; ++i) local += q_of(i);
+    int64_t total;
+    const int64_t pre = block_excl_scan(local, sml, total);
+    int kp_l = k;
+    {
+        int64_t c = pre;
+        for (int i = i0; i < i1; ++i) {
+            c += q_of(i);
+            if (c > (int64_t)R) {
+                kp_l = i;
+                break;
+            }
+        }
+    }
+    const int kp = block_min_int(kp_l, smi);
+    // cum at rank kp-1 (its chunk owner recomputes the running prefix)
+    auto cum_upto = [&](int i) -> int64_t {  // valid only for the owner of rank i
+        int64_t c = pre;
+        for (int t = i0; t <= i; ++t) c += q_of(t);
+        return c;
+    };
+    if (kp - 1 >= i0 && kp - 1 < i1) cum_at[0] = cum_upto(kp - 1);
+    __syncthreads();
+    const int64_t shift = (int64_t)R - cum_at[0] + (int64_t)st.lo;
+
+    // ---- selection
+    int sel_l = 0x7FFFFFFF;
+    uint32_t err = 0;
+    if (!DECODE) {
+        uint64_t idx = 0;
+        const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
+        const int64_t nbits = p.nbits[b];
+        for (int t = 0; t < p.P; ++t) {
+            const int64_t bp = st.bit_pos + t;
+            const uint32_t bit = bp < nbits ? ((pl[bp >> 3] >> (bp & 7)) & 1u) : 0u;
+            idx = (idx << 1) | bit;
+        }
+        int64_t c = pre;
+        for (int i = i0; i < min(i1, kp); ++i) {
+            c += q_of(i);
+            if ((uint64_t)(c + shift) > idx) {
+                sel_l = i;
+                break;
+            }
+        }
+    } else {
+        const int32_t tok = p.in_token[b];
+        if (tok >= 0 && tok < p.V && !is_banned(p, tok)) {
+            const uint64_t kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+            for (int i = i0; i < min(i1, kp); ++i)
+                if (sk[i] == kt) {
+                    sel_l = i;
+                    break;
+                }
+        }
+    }
+    const int sel = block_min_int(sel_l, smi);
+    if (sel == 0x7FFFFFFF) err = DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE;
+    if (!err) {
+        if (sel - 1 >= i0 && sel - 1 < i1) cum_at[1] = cum_upto(sel - 1);
+        if (sel >= i0 && sel < i1) cum_at[2] = cum_upto(sel);
+        if (tid == 0) sel_key = sk[sel];
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    if (err) {
+        p.state[b].flags = st.flags | err | NS_ST_DONE;
+        if (p.trace) {
+            ns_step_trace tr = {k, kp, -1, -1, -1, exact ? 1 : 0, S_used};
+            p.trace[b] = tr;
+        }
+        return;
+    }
+    const int P = p.P;
+    const uint64_t mask = (P >= 64) ? ~0ull : ((1ull << P) - 1ull);
+    const uint64_t new_lo = sel > 0 ? (uint64_t)(cum_at[1] + shift) : st.lo;
+    const uint64_t new_hi = (uint64_t)(cum_at[2] + shift);
+    const uint64_t top = new_hi - 1ull;
+    const uint64_t diff = (new_lo ^ top) & mask;
+    const int n = diff == 0ull ? P - 1 : P - (64 - __builtin_clzll(diff));
+    const int32_t token = (int32_t)wkey_id(sel_key);
+    ns_stream_state ns = st;
+    if (DECODE) {
+        const bool last = p.is_last[b] != 0;
+        const int cntb = last ? P : n;
+        const uint64_t src = last ? new_lo : top;
+        uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
+        for (int t = 0; t < cntb; ++t) {
+            const int64_t bp = st.bit_pos + t;
+            const uint8_t bitv = (uint8_t)((src >> (P - 1 - t)) & 1u);
+            const uint8_t bm = (uint8_t)(1u << (bp & 7));
+            ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | bm) : (uint8_t)(ob[bp >> 3] & ~bm);
+        }
+        ns.bit_pos = st.bit_pos + cntb;
+    } else {
+        ns.bit_pos = st.bit_pos + n;
+    }
+    ns.lo = (new_lo << n) & mask;
+    ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
+    ns.ntokens = st.ntokens + 1;
+    ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
+    if (!DECODE && ns.bit_pos >= p.nbits[b]) ns.flags |= NS_ST_DONE;
+    p.state[b] = ns;
+    if (!DECODE) {
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+    }
+    if (p.trace) {
+        ns_step_trace tr = {k, kp, sel, n, token, exact ? 1 : 0, S_used};
+        p.trace[b] = tr;
+    }
+    if (p.counters && exact) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1))], 1ull);
+}
+
+}  // namespace nsg
+
+// ------------------------------------------------------------------------------------------ host
+int nsg_wide_alloc(ns_ctx* ctx) {
+    NsgWide& w = ctx->wide;
+    if (w.keys_in) return NS_OK;
+    if (ctx->vocab > 0x1FFFF) return NS_ERR_UNSUPPORTED;
+    w.cap = ctx->vocab;
+    const size_t n = (size_t)ctx->max_batch * (size_t)w.cap;
+    if (hipMalloc((void**)&w.keys_in, n * 8) != hipSuccess || hipMalloc((void**)&w.keys_out, n * 8) != hipSuccess ||
+        hipMalloc((void**)&w.count, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void**)&w.begin, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void**)&w.end, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void**)&w.stat, ctx->max_batch * sizeof(nsg::WideStat)) != hipSuccess)
+        return NS_ERR_HIP;
+    size_t bytes = 0;
+    if (rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, w.keys_in, w.keys_out, (unsigned int)n,
+                                                (unsigned int)ctx->max_batch, w.begin, w.end, 0, 49) != hipSuccess)
+        return NS_ERR_HIP;
+    w.sort_tmp_bytes = bytes;
+    if (hipMalloc(&w.sort_tmp, bytes ? bytes : 16) != hipSuccess) return NS_ERR_HIP;
+    return NS_OK;
+}
+
+void nsg_wide_free(ns_ctx* ctx) {
+    NsgWide& w = ctx->wide;
+    for (void* ptr : {(void*)w.keys_in, (void*)w.keys_out, (void*)w.count, (void*)w.begin, (void*)w.end,
+                      (void*)w.stat, w.sort_tmp})
+        if (ptr) (void)hipFree(ptr);
+    w = NsgWide();
+}
+
+template <typename T, bool DECODE>
+static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
+    NsgWide& w = ctx->wide;
+    const int B = p.B;
+    hipLaunchKernelGGL((nsg::wide_stats_kernel<T, DECODE>), dim3((B + nsg::WPB - 1) / nsg::WPB),
+                       dim3(nsg::WPB * nsg::WAVE), 0, s, p, w.stat, w.count);
+    const int nchunk = (p.V + nsg::COLLECT_CHUNK - 1) / nsg::COLLECT_CHUNK;
+    hipLaunchKernelGGL((nsg::wide_collect_kernel<T>), dim3(nchunk, B), dim3(256), 0, s, p, w.stat, w.keys_in,
+                       w.count, w.cap);
+    hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
+                       w.count, w.begin, w.end);
+    size_t bytes = w.sort_tmp_bytes;
+    if (rocprim::segmented_radix_sort_keys_desc(w.sort_tmp, bytes, w.keys_in, w.keys_out,
+                                                (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin,
+                                                w.end, 0, 49, s) != hipSuccess)
+        return false;
+    hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B), dim3(nsg::WIDE_THREADS), 0, s, p, w.stat,
+                       w.keys_out, w.count, w.cap);
+    return hipGetLastError() == hipSuccess;
+}
+
+bool nsg_wide_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s) {
+    if (ctx->dtype == NS_DTYPE_F16)
+        return decode ? wide_launch_t<_Float16, true>(ctx, p, s) : wide_launch_t<_Float16, false>(ctx, p, s);
+    return decode ? wide_launch_t<float, true>(ctx, p, s) : wide_launch_t<float, false>(ctx, p, s);
+}

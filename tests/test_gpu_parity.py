@@ -17,6 +17,7 @@ from tests import golden
 pytestmark = pytest.mark.gpu
 
 KERNEL_GOLDEN = ["g1_v50257_f32_p26_k300", "g2_v50257_f16_p26_k100", "g3_v50257_f32_peaked_p26_k300",
+                 "g4_v50257_f32_p16_k50000", "g5_v50257_f32_p40_k60000",  # wide (large top-k) path
                  "g6_v700_f32_p20_k500", "g7_v640_f32_p12_k1000"]
 
 
@@ -70,11 +71,13 @@ def test_kernel_matches_reference_golden(name, force_exact):
         assert bt == s.bits, f"{name} stream {s.stream}: HIP decoded bits differ from the reference"
 
 
-def test_topk_beyond_single_pass_limit_is_loud():
+def test_wide_path_is_selected_beyond_single_pass_limit():
+    from neuralsteganography_amd import _lib
     from neuralsteganography_amd.coder import CoderParams
 
-    with pytest.raises(ConfigurationError):
-        _ctx(CoderParams(vocab=50257, precision=16, topk=50000), 2)
+    ctx = _ctx(CoderParams(vocab=50257, precision=16, topk=50000), 2)
+    assert ctx.wide and ctx.K == 50000 > _lib.max_topk(_lib.NS_DTYPE_F32)
+    assert not _ctx(CoderParams(vocab=50257, precision=26, topk=300), 2).wide
 
 
 def _oracle_step_traces(seed, stream, bits, params, scale, nsteps_cap=None):
@@ -92,12 +95,16 @@ def _oracle_step_traces(seed, stream, bits, params, scale, nsteps_cap=None):
     ("f32", 3.0, 1.0, 30, 768),    # the kernel's largest fp32 top-k
     ("f16", 1.0, 1.5, 20, 512),    # the kernel's largest fp16 top-k, flat rows
     ("f32", 0.05, 1.0, 26, 300),   # nearly uniform rows
+    ("f32", 3.0, 1.0, 16, 50000),  # wide path: api defaults (precision 16, topk 50000)
+    ("f16", 6.0, 0.9, 22, 2000),   # wide path, fp16, peaked: the cutoff binds inside the collected prefix
+    ("f32", 3.0, 0.9, 40, 60000),  # wide path, message->bits mode (run_single.py:52-54)
 ])
 def test_stepwise_traces_match_oracle(dtype, scale, temp, precision, topk):
     from neuralsteganography_amd.coder import CoderParams, EncodeSession, row_stride
 
     V, B, seed = 50257, 6, 11
     params = CoderParams(vocab=V, precision=precision, temp=temp, topk=topk, dtype=dtype)
+    force = topk > 768  # the wide path also runs its exact-sum branch every other step
     ctx = _ctx(params, B)
     ld = row_stride(V, dtype)
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 12))[: 96 - 7 * s] for s in range(B)]
@@ -107,7 +114,7 @@ def test_stepwise_traces_match_oracle(dtype, scale, temp, precision, topk):
     fn = _logits_fn(seed, list(range(B)), V, scale, dtype, ld)
     nmax = max(len(e[0]) for e in expect)
     for t in range(nmax):
-        sess.step(fn(t))
+        sess.step(fn(t), force_exact=force and t % 2 == 1)
         tr = sess.trace_rows()
         for s in range(B):
             if t < len(expect[s][1]):
