@@ -54,6 +54,8 @@ extern "C" {
 
 /* step flags */
 #define NS_STEP_FORCE_EXACT_SUM 1u /* always take the exact-sum path (parity testing) */
+#define NS_STEP_FINISH_SENT 16u /* encode: after the payload, emit top-1 tokens until a sentence end
+                                   (code_base/arithmetic.py:114,134-137); needs ns_set_sentence_end   */
 /* diagnostic flags for phase timing only: the step does NOT advance any state when one is set */
 #define NS_STEP_DIAG_STREAM_ONLY 2u    /* stop after the streaming pass                           */
 #define NS_STEP_DIAG_NO_CANDIDATES 4u  /* streaming pass without candidate collection, then stop  */
@@ -116,6 +118,11 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
                    const uint8_t* d_is_last, const uint8_t* d_active, ns_stream_state* d_state,
                    uint8_t* d_out_bits, int64_t out_stride, double temp, int topk, const int32_t* banned,
                    int nbanned, ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
+
+/* Register the sentence-end table used by NS_STEP_FINISH_SENT: d_table is a DEVICE array of `vocab`
+ * bytes, nonzero for ids whose text contains '.', '!' or '?' (code_base/utils.py:55-57,
+ * is_sent_finish).  The caller keeps it alive; NULL clears it. */
+int ns_set_sentence_end(ns_ctx* ctx, const uint8_t* d_table);
 
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses

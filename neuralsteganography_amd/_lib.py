@@ -21,11 +21,12 @@ NS_OK, NS_ERR_CONFIG, NS_ERR_UNSUPPORTED, NS_ERR_HIP = 0, -1, -2, -3
 NS_DTYPE_F32, NS_DTYPE_F16 = 0, 1
 NS_ST_DONE, NS_ST_ERR_RANGE, NS_ST_ERR_DIVERGE, NS_ST_EXACT_SUM = 1, 2, 4, 8
 NS_STEP_FORCE_EXACT_SUM = 1
+NS_STEP_FINISH_SENT = 16
 NS_STEP_DIAG_STREAM_ONLY, NS_STEP_DIAG_NO_CANDIDATES, NS_STEP_DIAG_SKIP_CDF = 2, 4, 8
 NS_MAX_BANNED = 8
 
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
-           "ns_encode_step", "ns_decode_step", "ns_read_counters")
+           "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_read_counters")
 
 
 class NsStreamState(ctypes.Structure):
@@ -79,6 +80,8 @@ def lib() -> ctypes.CDLL:
     L.ns_decode_step.restype = ctypes.c_int
     L.ns_decode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int64,
                                  ctypes.c_double, ctypes.c_int, i32p, ctypes.c_int, vp, ctypes.c_uint32, vp]
+    L.ns_set_sentence_end.restype = ctypes.c_int
+    L.ns_set_sentence_end.argtypes = [vp, vp]
     L.ns_read_counters.restype = ctypes.c_int
     L.ns_read_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     _lib = L

@@ -117,6 +117,19 @@ class CoderContext:
                 raise ConfigurationError(f"{what}: {msg}")
             raise _lib.NativeLibraryError(f"{what}: rc={rc}: {msg}")
 
+    def set_sentence_end(self, table) -> None:
+        """Register a device uint8 table [vocab] (nonzero = sentence-ending token) for finish_sent."""
+        torch = _torch()
+        if table is None:
+            self._sent_end = None
+            self.check(_lib.lib().ns_set_sentence_end(self._h, ctypes.c_void_p(0)), "ns_set_sentence_end")
+            return
+        t = torch.as_tensor(table, dtype=torch.uint8).to(torch.device("cuda", self.device)).contiguous()
+        if t.numel() != self.params.vocab:
+            raise ConfigurationError("sentence-end table must have one entry per vocabulary id")
+        self._sent_end = t  # keep alive: the library holds the raw pointer
+        self.check(_lib.lib().ns_set_sentence_end(self._h, _ptr(t)), "ns_set_sentence_end")
+
     def counters(self) -> List[int]:
         out = (ctypes.c_uint64 * 4)()
         self.check(_lib.lib().ns_read_counters(self._h, out), "ns_read_counters")
@@ -179,13 +192,17 @@ class EncodeSession:
         self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
         return self.trace
 
-    def step(self, logits, *, force_exact: bool = False, diag_flags: int = 0):
+    def step(self, logits, *, force_exact: bool = False, finish_sent: bool = False, diag_flags: int = 0):
         """One coder step on ``logits`` ([B, ld] contiguous rows, ld = :func:`row_stride`).
 
-        ``diag_flags`` (NS_STEP_DIAG_*) are for phase timing only: such a step advances no state."""
+        ``finish_sent``: once a stream's payload is consumed it keeps emitting top-1 tokens until a
+        sentence-ending one (needs :meth:`CoderContext.set_sentence_end`).  ``diag_flags``
+        (NS_STEP_DIAG_*) are for phase timing only: such a step advances no state."""
         p = self.ctx.params
         self._check_logits(logits)
         flags = (_lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0) | int(diag_flags)
+        if finish_sent:
+            flags |= _lib.NS_STEP_FINISH_SENT
         rc = _lib.lib().ns_encode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
             _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), self.hist.shape[1],
@@ -204,6 +221,17 @@ class EncodeSession:
 
     def all_done(self) -> bool:
         return bool(np.all(_state_fields(self.state)["flags"] & _lib.NS_ST_DONE))
+
+    def ensure_history(self, steps_ahead: int) -> None:
+        """Grow the device token history so ``steps_ahead`` more steps fit (finish_sent tails are unbounded)."""
+        need = int(self.fields()["ntokens"].max(initial=0)) + int(steps_ahead)
+        cap = self.hist.shape[1]
+        if need <= cap:
+            return
+        torch = _torch()
+        new = torch.full((self.B, max(need, 2 * cap)), -1, dtype=torch.int32, device=self.hist.device)
+        new[:, :cap] = self.hist
+        self.hist = new
 
     def fields(self) -> dict:
         return _state_fields(self.state)
@@ -294,15 +322,17 @@ class DecodeSession:
 
 
 def encode_batch(ctx: CoderContext, payload_bits: Sequence[Sequence[int]], logits_fn, *, max_steps: int = 1 << 20,
-                 check_every: int = 32, force_exact: bool = False) -> List[List[int]]:
+                 check_every: int = 32, force_exact: bool = False, finish_sent: bool = False) -> List[List[int]]:
     """Run encode steps until every stream has consumed its payload; ``logits_fn(step, last_tokens)``
     returns the ``[B, ld]`` logits of that step."""
     sess = EncodeSession(ctx, payload_bits)
     last = sess.out_token
     for t in range(max_steps):
-        if t % check_every == 0 and sess.all_done():
-            break
-        last = sess.step(logits_fn(t, last), force_exact=force_exact)
+        if t % check_every == 0:
+            if sess.all_done():
+                break
+            sess.ensure_history(check_every)
+        last = sess.step(logits_fn(t, last), force_exact=force_exact, finish_sent=finish_sent)
     else:
         raise ConfigurationError("encode did not finish within max_steps")
     return sess.tokens()

@@ -224,8 +224,8 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     int64_t nbits = 0;
     if (!DECODE) {
         nbits = p.nbits[b];
-        if (st.bit_pos >= nbits) {
-            if (lane == 0) p.state[b].flags = st.flags | NS_ST_DONE;
+        if (st.bit_pos >= nbits) {  // payload consumed: done, or sentence finishing (finish_sent_kernel)
+            if (lane == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
             return;
         }
     } else {
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
         ns.ntokens = st.ntokens + 1;
         ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
-        if (!DECODE && ns.bit_pos >= nbits) ns.flags |= NS_ST_DONE;
+        if (!DECODE && ns.bit_pos >= nbits && !(p.flags & NS_STEP_FINISH_SENT)) ns.flags |= NS_ST_DONE;
         if (lane == 0) {
             p.state[b] = ns;
             if (!DECODE) {
@@ -629,6 +629,52 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         if (exact) atomicAdd(&c[0], 1ull);
         if (overflow > 0) atomicAdd(&c[1], (unsigned long long)overflow);
         if (nfallback) atomicAdd(&c[2], (unsigned long long)nfallback);
+    }
+}
+
+// finish_sent (code_base/arithmetic.py:114,134-137): once the payload is consumed, emit the top-1 token
+// (rank 0: max value, lowest id) each step until a sentence-ending token; the interval is left untouched.
+template <typename T>
+__global__ __launch_bounds__(WPB* WAVE) void finish_sent_kernel(StepParams p, const uint8_t* sent_end) {
+    constexpr int W = Elem<T>::W;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + (int)(threadIdx.x / WAVE));
+    if (b >= p.B) return;
+    const ns_stream_state st = p.state[b];
+    if ((st.flags & NS_ST_DONE) || st.bit_pos < p.nbits[b]) return;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int nvec = (p.V + W - 1) / W;
+    uint64_t best = 0;  // max (value desc, id asc) key
+    for (int v = lane; v < nvec; v += WAVE) {
+        float x[W];
+        Elem<T>::unpack(rd.vec(v), x);
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            const int j = v * W + q;
+            if (j < p.V && !is_banned(p, j)) {
+                const uint64_t k = make_key(x[q], (uint32_t)j);
+                best = k > best ? k : best;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if (lane == 0) {
+        const int32_t token = (int32_t)key_id(best);
+        ns_stream_state ns = st;
+        ns.ntokens = st.ntokens + 1;
+        if (sent_end[token]) ns.flags |= NS_ST_DONE;
+        p.state[b] = ns;
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        if (p.trace) {
+            ns_step_trace tr = {0, 0, 0, 0, token, 0, 0.0};
+            p.trace[b] = tr;
+        }
     }
 }
 
@@ -697,7 +743,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.4 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.5 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -729,6 +775,7 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->dtype = logits_dtype;
     ctx->d_counters = nullptr;
     ctx->wide = NsgWide();
+    ctx->sent_end = nullptr;
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
@@ -835,6 +882,14 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
     p.out_token = d_out_token;
     p.hist = d_token_hist;
     p.hist_stride = d_token_hist ? hist_stride : 0;
+    if (step_flags & NS_STEP_FINISH_SENT) {
+        if (!ctx->sent_end) return fail(ctx, NS_ERR_CONFIG, "NS_STEP_FINISH_SENT needs ns_set_sentence_end");
+        const dim3 g((B + nsg::WPB - 1) / nsg::WPB), blk(nsg::WPB * nsg::WAVE);
+        if (ctx->dtype == NS_DTYPE_F16)
+            hipLaunchKernelGGL(nsg::finish_sent_kernel<_Float16>, g, blk, 0, (hipStream_t)hip_stream, p, ctx->sent_end);
+        else
+            hipLaunchKernelGGL(nsg::finish_sent_kernel<float>, g, blk, 0, (hipStream_t)hip_stream, p, ctx->sent_end);
+    }
     const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, false, (hipStream_t)hip_stream)
                                                   : launch<false>(ctx, p, (hipStream_t)hip_stream);
     if (!ok) return fail(ctx, NS_ERR_HIP, "ns_encode_step: launch failed");
@@ -858,6 +913,12 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
     const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, true, (hipStream_t)hip_stream)
                                                   : launch<true>(ctx, p, (hipStream_t)hip_stream);
     if (!ok) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
+    return NS_OK;
+}
+
+int ns_set_sentence_end(ns_ctx* ctx, const uint8_t* d_table) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "ns_set_sentence_end: null context");
+    ctx->sent_end = d_table;
     return NS_OK;
 }
 

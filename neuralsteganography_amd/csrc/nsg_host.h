@@ -46,6 +46,7 @@ struct ns_ctx {
     int dtype;
     unsigned long long* d_counters;
     NsgWide wide;
+    const uint8_t* sent_end;  // device table [vocab] for NS_STEP_FINISH_SENT (ns_set_sentence_end)
     std::string err;
 };
 

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
     const ns_stream_state st = p.state[b];
     bool active = !(st.flags & NS_ST_DONE);
     if (!DECODE && active && st.bit_pos >= p.nbits[b]) {
-        if (lane == 0) p.state[b].flags = st.flags | NS_ST_DONE;
+        if (lane == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
         active = false;
     }
     if (DECODE && p.active && !p.active[b]) active = false;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
     ns.ntokens = st.ntokens + 1;
     ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
-    if (!DECODE && ns.bit_pos >= p.nbits[b]) ns.flags |= NS_ST_DONE;
+    if (!DECODE && ns.bit_pos >= p.nbits[b] && !(p.flags & NS_STEP_FINISH_SENT)) ns.flags |= NS_ST_DONE;
     p.state[b] = ns;
     if (!DECODE) {
         p.out_token[b] = token;

@@ -91,6 +91,7 @@ class HipArithmeticLM:
         self.max_batch = int(max_batch)
         self.device = dev
         self._ctx_cache: Dict[tuple, CoderContext] = {}
+        self._sent_end = None
         self._encode_states: List[CodecState] = []
         self._decode_states: Deque[CodecState] = deque()
 
@@ -103,6 +104,23 @@ class HipArithmeticLM:
             ctx = CoderContext(params, max_batch=max(B, 1), device=self.device.index)
             self._ctx_cache[key] = ctx
         return ctx
+
+    def sentence_end_table(self):
+        """Per-id table of sentence-ending tokens: ``'.' in t or '!' in t or '?' in t`` for the decoded
+        text of each id (``code_base/utils.py:55-57``)."""
+        if self._sent_end is None:
+            import numpy as np
+
+            tab = np.zeros(self.vocab, dtype=np.uint8)
+            for i in range(self.vocab):
+                try:
+                    txt = self.tokenizer.decode([i])
+                except Exception:
+                    continue
+                if "." in txt or "!" in txt or "?" in txt:
+                    tab[i] = 1
+            self._sent_end = tab
+        return self._sent_end
 
     # ---------------------------------------------------------------- protocol
     def encode_seed(self, text: str) -> List[int]:
@@ -155,6 +173,9 @@ class HipArithmeticLM:
             return []
         params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
         ctx = self._coder(params, B)
+        finish = bool(dict(quality or {}).get("finish_sent", False))
+        if finish:
+            ctx.set_sentence_end(self.sentence_end_table())
         max_bits = max(len(b) for b in bit_lists)
         budget = 2 * max_bits + 64            # initial KV/history capacity (grows on demand)
         hard_cap = 64 * max_bits + 4096       # a stream fixing < 1/64 bit per token is reported, not looped
@@ -170,18 +191,20 @@ class HipArithmeticLM:
                     break
                 pos = f["bit_pos"].copy()
                 if last_pos is None or (pos != last_pos).any():
-                    moved = last_pos is None or (pos != last_pos)
                     last_pos, last_move = pos, t
-                    _ = moved
                 if t - last_move >= stall_steps or t >= hard_cap:
                     from ..codec.errors import ArithmeticRangeError
 
                     stuck = [i for i in range(B) if not (f["flags"][i] & 1)]
+                    if all(f["bit_pos"][i] >= len(bit_lists[i]) for i in stuck):
+                        raise ArithmeticRangeError(
+                            f"finish_sent: streams {stuck[:8]} produced no sentence-ending token in "
+                            f"{t - last_move} tokens (the reference would keep generating forever)")
                     raise ArithmeticRangeError(
                         f"streams {stuck[:8]} fixed no payload bit for {t - last_move} tokens: the interval "
                         "straddles the midpoint and one token takes the whole range (the reference coder "
                         "has no underflow handling and would loop forever)")
-            tok = sess.step(logits)
+            tok = sess.step(logits, finish_sent=finish)
             logits = self.lm.step(tok)
             t += 1
         toks = sess.tokens()

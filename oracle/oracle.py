@@ -132,8 +132,11 @@ RowFn = Callable[[int], np.ndarray]
 
 
 def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, precision: int, topk: int,
-                  max_steps: int = 1 << 20) -> Tuple[List[int], List[OrTrace]]:
-    """Encode one bit list (``code_base/arithmetic.py:112-210`` loop); ``row_fn(t)`` gives step t's logits."""
+                  max_steps: int = 1 << 20, sent_end=None) -> Tuple[List[int], List[OrTrace]]:
+    """Encode one bit list (``code_base/arithmetic.py:112-210`` loop); ``row_fn(t)`` gives step t's logits.
+
+    ``sent_end`` (a per-id boolean table) enables finish_sent (``:114,134-137``): after the payload, the
+    top-1 token (max logit, lowest id, banned excluded) is emitted until one is sentence-ending."""
     nbits = len(bits)
     packed = np.packbits(np.asarray(bits, dtype=np.uint8), bitorder="little") if nbits else np.zeros(1, np.uint8)
     st = new_state(precision)
@@ -149,6 +152,18 @@ def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, pr
         toks.append(tok)
         traces.append(tr)
         t += 1
+    if sent_end is not None:
+        while True:
+            if t >= max_steps:
+                raise RuntimeError("oracle finish_sent did not terminate")
+            row = np.asarray(row_fn(t), dtype=np.float32).copy()
+            row[list(banned)] = -np.inf
+            row = row + np.float32(0.0)  # -0 -> +0, as the canonical key
+            tok = int(np.flatnonzero(row == row.max())[0])
+            toks.append(tok)
+            t += 1
+            if sent_end[tok]:
+                break
     return toks, traces
 
 

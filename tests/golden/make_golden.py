@@ -81,11 +81,16 @@ class SyntheticModel:
 
 
 class StubTokenizer:
-    def __init__(self, tokens=None):
+    """decode(): "." for sentence-ending ids (id % 97 == 5 when `finish` is set), else "a"; never '<eos>'."""
+
+    def __init__(self, tokens=None, finish=False):
         self.tokens = list(tokens or [])
+        self.finish = finish
 
     def decode(self, ids):
-        return ""
+        if not self.finish:
+            return ""
+        return "".join("." if int(i) % 97 == 5 else "a" for i in ids)
 
     def encode(self, text):
         return list(self.tokens)
@@ -114,6 +119,9 @@ CONFIGS = {
     # topk above the non-banned count: every candidate kept.
     "g7_v640_f32_p12_k1000": dict(vocab=640, dtype="f32", scale=1.0, temp=1.3, precision=12, topk=1000,
                                   nbits=[200, 64]),
+    # finish_sent=True (code_base/arithmetic.py:114,134-137): sentence-ending ids are id % 97 == 5.
+    "g8_v50257_f32_p26_k300_finish": dict(vocab=50257, dtype="f32", scale=3.0, temp=0.9, precision=26, topk=300,
+                                          nbits=[96, 64, 40, 8], finish_sent=True),
 }
 
 LOGIT_SEED = 7
@@ -130,15 +138,16 @@ def run_config(name, cfg, ref, stable_sort_mode):
         nbytes = (nbits + 7) // 8
         msg = synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes))[:nbits]
         model = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], dtype)
+        finish = bool(cfg.get("finish_sent", False))
         with stable_sort_mode():
             toks, nll, kl_, wpb, hq = ref.encode_arithmetic(
-                model, StubTokenizer(), list(msg), context, device="cpu", temp=cfg["temp"],
-                precision=cfg["precision"], topk=cfg["topk"])
+                model, StubTokenizer(finish=finish), list(msg), context, finish_sent=finish, device="cpu",
+                temp=cfg["temp"], precision=cfg["precision"], topk=cfg["topk"])
         nsteps = model.calls
         assert nsteps == len(toks)
         dmodel = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], dtype)
         with stable_sort_mode():
-            bits = ref.decode_arithmetic(dmodel, StubTokenizer(toks), "", context, device="cpu",
+            bits = ref.decode_arithmetic(dmodel, StubTokenizer(toks, finish=finish), "", context, device="cpu",
                                          temp=cfg["temp"], precision=cfg["precision"], topk=cfg["topk"])
         assert bits[:nbits] == msg, f"{name} stream {s}: reference round trip failed"
         tie_free = all(synthetic.top_region_tie_free(

@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 KERNEL_GOLDEN = ["g1_v50257_f32_p26_k300", "g2_v50257_f16_p26_k100", "g3_v50257_f32_peaked_p26_k300",
                  "g4_v50257_f32_p16_k50000", "g5_v50257_f32_p40_k60000",  # wide (large top-k) path
-                 "g6_v700_f32_p20_k500", "g7_v640_f32_p12_k1000"]
+                 "g6_v700_f32_p20_k500", "g7_v640_f32_p12_k1000",
+                 "g8_v50257_f32_p26_k300_finish"]  # finish_sent=True
 
 
 def _torch():
@@ -63,7 +64,9 @@ def test_kernel_matches_reference_golden(name, force_exact):
     ctx = _ctx(params, B)
     ld = row_stride(m["vocab"], m["dtype"])
     fn = _logits_fn(m["logit_seed"], [s.stream for s in g.streams], m["vocab"], m["scale"], m["dtype"], ld)
-    toks = encode_batch(ctx, [s.msg for s in g.streams], fn, force_exact=force_exact)
+    if g.finish_sent:
+        ctx.set_sentence_end(g.sent_end_table())
+    toks = encode_batch(ctx, [s.msg for s in g.streams], fn, force_exact=force_exact, finish_sent=g.finish_sent)
     for s, tk in zip(g.streams, toks):
         assert tk == s.tokens, f"{name} stream {s.stream}: HIP tokens differ from the reference"
     bits = decode_batch(ctx, [s.tokens for s in g.streams], fn, force_exact=force_exact)
@@ -122,6 +125,44 @@ def test_stepwise_traces_match_oracle(dtype, scale, temp, precision, topk):
                 assert got == expect[s][1][t], f"stream {s} step {t}: kernel {got} oracle {expect[s][1][t]}"
     assert sess.all_done()
     assert sess.tokens() == [e[0] for e in expect]
+
+
+@pytest.mark.parametrize("dtype,precision,topk", [
+    ("f32", 26, 300),      # single-pass kernel
+    ("f16", 26, 100),
+    ("f32", 16, 50000),    # wide path
+])
+def test_finish_sent_matches_oracle(dtype, precision, topk):
+    """finish_sent (code_base/arithmetic.py:114,134-137): after the payload, top-1 tokens until one is
+    sentence-ending; ragged payloads so streams sit in different phases of the same launch."""
+    from neuralsteganography_amd.coder import CoderParams, encode_batch, row_stride
+
+    V, B, seed, scale = 50257, 5, 23, 3.0
+    params = CoderParams(vocab=V, precision=precision, temp=0.9, topk=topk, dtype=dtype)
+    ctx = _ctx(params, B)
+    table = (np.arange(V) % 211 == 17).astype(np.uint8)   # sparse: long top-1 tails
+    ctx.set_sentence_end(table)
+    ld = row_stride(V, dtype)
+    npdt = np.float16 if dtype == "f16" else np.float32
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 8))[: [64, 1, 0, 33, 7][s]] for s in range(B)]
+    toks = encode_batch(ctx, bits, _logits_fn(seed, list(range(B)), V, scale, dtype, ld), finish_sent=True,
+                        check_every=8)
+    for s in range(B):
+        row = lambda t, s=s: synthetic.logits_row(seed, s, t, V, scale, npdt).astype(np.float32)
+        ref, _ = oracle.encode_stream(row, bits[s], banned=params.banned_ids(), temp=0.9, precision=precision,
+                                      topk=topk, sent_end=table)
+        assert toks[s] == ref, f"stream {s}: finish_sent tokens differ from the oracle"
+        assert table[toks[s][-1]], f"stream {s}: the finish tail must end on a sentence-ending token"
+
+
+def test_finish_sent_needs_table():
+    from neuralsteganography_amd.coder import CoderParams, encode_batch, row_stride
+
+    V = 50257
+    ctx = _ctx(CoderParams(vocab=V, precision=26, temp=0.9, topk=300), 2)
+    fn = _logits_fn(1, [0, 1], V, 3.0, "f32", row_stride(V, "f32"))
+    with pytest.raises(ConfigurationError):
+        encode_batch(ctx, [[1, 0], [1]], fn, finish_sent=True)
 
 
 def test_roundtrip_large_batch_properties():

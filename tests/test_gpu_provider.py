@@ -114,3 +114,54 @@ def test_reference_stall_is_reported_not_hung():
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 4)) for s in range(2)]
     with pytest.raises(ArithmeticRangeError):
         lm.encode_batch(bits, [1999], quality={"temp": 1.0, "precision": 26, "topk": 300}, stall_steps=64)
+
+
+def test_provider_finish_sent_matches_oracle():
+    """quality['finish_sent'] (code_base/arithmetic.py:114,134-137): the LM loop keeps emitting top-1 tokens
+    after the payload until a sentence-ending one; the coder's choices inside the loop equal the oracle's
+    replay on the captured logits, and decode recovers the payload from the longer cover."""
+    _, lm = _tiny_provider()
+    V = lm.vocab
+    # random tied-embedding LMs fall into greedy fixed points, so the table marks most ids (tails stay short);
+    # long tails are covered on synthetic rows in test_gpu_parity.test_finish_sent_matches_oracle
+    table = (np.arange(V) % 8 != 3).astype(np.uint8)
+    lm._sent_end = table
+    quality = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": True}
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 6))[: [48, 5, 0][s]] for s in range(3)]
+    context = lm.encode_seed("finish")
+    seen = []
+    orig_step, orig_prefill = lm.lm.step, lm.lm.prefill
+
+    def rec_prefill(*a, **k):
+        out = orig_prefill(*a, **k)
+        seen.append(out.float().cpu().numpy().copy())
+        return out
+
+    def rec_step(tok):
+        out = orig_step(tok)
+        seen.append(out.float().cpu().numpy().copy())
+        return out
+
+    lm.lm.prefill, lm.lm.step = rec_prefill, rec_step
+    toks = lm.encode_batch(bits, context, quality=quality, stall_steps=512)
+    lm.lm.prefill, lm.lm.step = orig_prefill, orig_step
+    for s in range(3):
+        o, _ = oracle.encode_stream(lambda t: seen[t][s, :V], bits[s], banned=[V - 1, 628], temp=0.9,
+                                    precision=26, topk=300, sent_end=table)
+        assert o == toks[s], f"stream {s}: finish_sent inside the LM loop differs from the oracle"
+        assert table[toks[s][-1]]
+    out = lm.decode_batch([t for t in toks if t], context, quality=quality)
+    for b, got in zip([b for b, t in zip(bits, toks) if t], out):
+        assert got[: len(b)] == b
+
+
+def test_provider_finish_sent_without_sentence_end_is_reported():
+    """No id ends a sentence: the reference would generate forever; the provider raises after stall_steps."""
+    from neuralsteganography_amd.codec.errors import ArithmeticRangeError
+
+    _, lm = _tiny_provider()
+    lm._sent_end = np.zeros(lm.vocab, dtype=np.uint8)
+    bits = [synthetic.bytes_to_bits_lsb(b"\x05")]
+    with pytest.raises(ArithmeticRangeError, match="finish_sent"):
+        lm.encode_batch(bits, lm.encode_seed(""), quality={"temp": 1.0, "precision": 20, "topk": 100,
+                                                            "finish_sent": True}, stall_steps=64)

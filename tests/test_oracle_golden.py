@@ -19,8 +19,9 @@ def test_oracle_matches_reference_golden(name):
     m = g.meta
     for s in g.streams:
         row = lambda t, s=s: g.row(s.stream, t).astype(np.float32)
+        sent_end = g.sent_end_table() if g.finish_sent else None
         toks, _ = oracle.encode_stream(row, s.msg, banned=m["banned"], temp=m["temp"], precision=m["precision"],
-                                       topk=m["topk"])
+                                       topk=m["topk"], sent_end=sent_end)
         assert toks == s.tokens, f"{name} stream {s.stream}: encode tokens differ from the reference"
         bits, _ = oracle.decode_stream(row, s.tokens, banned=m["banned"], temp=m["temp"],
                                        precision=m["precision"], topk=m["topk"])
@@ -49,7 +50,8 @@ def test_exp_canon_accuracy():
 
 def test_golden_fixtures_cover_the_configs():
     names = golden.names()
-    assert len(names) >= 7
+    assert len(names) >= 8
+    assert any(golden.load(n).finish_sent for n in names)
     g = golden.load("g1_v50257_f32_p26_k300")
     assert g.meta["precision"] == 26 and g.meta["topk"] == 300 and g.meta["temp"] == 0.9
     # ragged payload lengths including 1 bit
