@@ -126,7 +126,8 @@ int ns_set_sentence_end(ns_ctx* ctx, const uint8_t* d_table);
 
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
- * (row re-read), counters[3] = reserved.  Synchronises the device. */
+ * (row re-read), counters[3] = top-K selections that left the histogram fast path (value ties or a skewed
+ * row: bisection compaction or full-count ranking).  Synchronises the device. */
 int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters4);
 
 #ifdef __cplusplus

@@ -36,11 +36,24 @@
 #include "nsg_host.h"
 #include "nsg_host.h"
 
+#ifndef NSG_BUCKET_CAP
+#define NSG_BUCKET_CAP 48  // largest bucket the bucket rank accepts (its fix-up loop runs that often)
+#endif
+
 namespace nsg {
 
+// Per-wave LDS scratch: 256+4 bucket counters/bases (u32), 64 gathered keys (u64), and a slow-path counter.
+constexpr int SCR_U32 = 392;
+constexpr int SCR_GATHER = 260;  // u32 offset of the gather area (8-byte aligned)
+constexpr int SCR_SLOW = 391;    // selections that fell back to bisection / full counting (counters[3])
+
+__device__ __forceinline__ void note_slow(uint32_t* scr, int lane) {
+    if (lane == 0) scr[SCR_SLOW] += 1u;
+}
+
 // Keep exactly the top-K keys of keys[0..cnt) (cnt >= K).  Bisection on the value word, then on the id
-// word among ties; counts by ballot+popcount.  Returns the K-th key.
-__device__ __noinline__ uint64_t compact_topk(uint64_t* keys, int cnt, int K, int lane) {
+// word among ties; counts by ballot+popcount.  Returns the K-th key.  (Fallback of compact_topk.)
+__device__ __noinline__ uint64_t compact_bisect(uint64_t* keys, int cnt, int K, int lane) {
     constexpr int NSL = CAND / WAVE;
     uint64_t kr[NSL];
 #pragma unroll
@@ -95,10 +108,112 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, int cnt, int K, in
     return kappa;
 }
 
+// Keep exactly the top-K keys of keys[0..cnt) (cnt >= K); returns the K-th key.  Histogram select: the
+// value words are bucketed by a digit monotone in the value (256 linear buckets over [min, max], largest
+// first, LDS ds_add), a scan finds the bucket holding the K-th key, only that bucket's keys are ranked
+// exactly, and everything at or above the K-th key is kept.  Keys are re-read from LDS in every pass (few
+// live registers: this is called from inside the streaming loop).  Falls back to bisection when every key
+// has the same value word or the boundary bucket holds more than 64 keys.
+__device__ __noinline__ uint64_t compact_topk(uint64_t* keys, uint32_t* scr, int cnt, int K, int lane) {
+    constexpr int NB = 256;
+    const int nsl = (cnt + WAVE - 1) / WAVE;
+    uint32_t hmin = 0xFFFFFFFFu, hmax = 0u;
+#pragma unroll 4
+    for (int s = 0; s < nsl; ++s) {
+        const int i = s * WAVE + lane;
+        if (i < cnt) {
+            const uint32_t h = (uint32_t)(keys[i] >> 32);
+            hmin = min(hmin, h);
+            hmax = max(hmax, h);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        hmin = min(hmin, (uint32_t)__shfl_xor((int)hmin, off));
+        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+    }
+    hmin = __builtin_amdgcn_readfirstlane(hmin);
+    hmax = __builtin_amdgcn_readfirstlane(hmax);
+    if (hmax == hmin) {
+        note_slow(scr, lane);
+        return compact_bisect(keys, cnt, K, lane);
+    }
+    const float scale = __uint_as_float(
+        __builtin_amdgcn_readfirstlane(__float_as_uint(255.99f / (float)(hmax - hmin))));  // wave-uniform
+    // bucket of a key, largest values first (digit monotone in the value word; two roundings keep it < 256)
+    auto bucket = [&](uint64_t k) -> uint32_t {
+        return (uint32_t)(NB - 1) -
+               min((uint32_t)((float)((uint32_t)(k >> 32) - hmin) * scale), (uint32_t)(NB - 1));
+    };
+    reinterpret_cast<uint4*>(scr)[lane] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 4
+    for (int s = 0; s < nsl; ++s) {
+        const int i = s * WAVE + lane;
+        if (i < cnt) atomicAdd(&scr[bucket(keys[i])], 1u);
+    }
+    lds_fence();
+    const uint4 c4 = reinterpret_cast<const uint4*>(scr)[lane];
+    const uint32_t i1 = c4.x, i2 = i1 + c4.y, i3 = i2 + c4.z, i4 = i3 + c4.w;
+    uint32_t inc = i4;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
+        if (lane >= off) inc += y;
+    }
+    const uint32_t ex = inc - i4;
+    // the bucket holding the K-th key: A < K <= A + C (exactly one, since cnt >= K)
+    int hit = -1;
+    uint32_t a_hit = 0u, c_hit = 0u;
+    if (ex < (uint32_t)K && ex + c4.x >= (uint32_t)K) { hit = 0; a_hit = ex; c_hit = c4.x; }
+    if (ex + i1 < (uint32_t)K && ex + i2 >= (uint32_t)K) { hit = 1; a_hit = ex + i1; c_hit = c4.y; }
+    if (ex + i2 < (uint32_t)K && ex + i3 >= (uint32_t)K) { hit = 2; a_hit = ex + i2; c_hit = c4.z; }
+    if (ex + i3 < (uint32_t)K && ex + i4 >= (uint32_t)K) { hit = 3; a_hit = ex + i3; c_hit = c4.w; }
+    const int src = (int)__builtin_ctzll(ballot(hit >= 0));
+    const uint32_t bstar = __builtin_amdgcn_readlane(4 * lane + hit, src);
+    const uint32_t astar = __builtin_amdgcn_readlane(a_hit, src);
+    const uint32_t hstar = __builtin_amdgcn_readlane(c_hit, src);
+    if (hstar > (uint32_t)WAVE) {
+        note_slow(scr, lane);
+        return compact_bisect(keys, cnt, K, lane);
+    }
+    const int need = K - (int)astar;  // 1 <= need <= hstar
+    uint64_t* g = reinterpret_cast<uint64_t*>(scr + SCR_GATHER);
+    int gb = 0;
+#pragma unroll 4
+    for (int s = 0; s < nsl; ++s) {
+        const int i = s * WAVE + lane;
+        const uint64_t k = i < cnt ? keys[i] : 0ull;
+        const bool in = k != 0ull && bucket(k) == bstar;
+        const uint64_t m = ballot(in);
+        if (in) g[gb + lanes_below(m)] = k;
+        gb += popc64(m);
+    }
+    lds_fence();
+    const uint64_t mine = lane < (int)hstar ? g[lane] : 0ull;
+    int r = 0;
+    for (uint32_t t = 0; t < hstar; ++t) r += g[t] > mine ? 1 : 0;  // LDS broadcast reads
+    const uint64_t mk = ballot(lane < (int)hstar && r == need - 1);
+    const uint64_t kappa = __shfl(mine, (int)__builtin_ctzll(mk));
+    // in-place keep: slot s's keys are read before any write, and writes land below (s+1)*64
+    int base = 0;
+#pragma unroll 4
+    for (int s = 0; s < nsl; ++s) {
+        const int i = s * WAVE + lane;
+        const uint64_t k = i < cnt ? keys[i] : 0ull;
+        const bool keep = k >= kappa && k != 0ull;
+        const uint64_t m = ballot(keep);
+        if (keep) keys[base + lanes_below(m)] = k;
+        base += popc64(m);
+    }
+    lds_fence();
+    return kappa;
+}
+
 // buffer-resource row reader: one SRD per wave (uniform), range-checked 16-byte loads (0 beyond the row)
 // Candidate buffer of one wave: keys of every element > thr seen so far (a superset of the running top-K).
 struct Cand {
     uint64_t* keys;
+    uint32_t* scr;  // per-wave LDS scratch (SCR_U32)
     int cnt;
     int ncompact;
     float thr;  // element passes iff x > thr
@@ -118,7 +233,7 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
         npt += popc64(msk[q]);
     }
     if (c.cnt + npt > CAND) {  // cnt > CAND - TS >= K: keep the exact running top-K
-        const uint64_t kappa = compact_topk(c.keys, c.cnt, K, lane);
+        const uint64_t kappa = compact_topk(c.keys, c.scr, c.cnt, K, lane);
         ++c.ncompact;
         c.cnt = K;
         // later elements have larger ids than every buffered key, so ties at the K-th value rank below it
@@ -187,6 +302,98 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
     c.cnt += total;
 }
 
+// Rank the K unique keys held in sk[] (key i = s*64 + lane) and store keys[rank] = key (rank 0 = largest).
+// Bucket pass: a digit monotone in the value word (256 linear buckets over [min, max] of the value words,
+// largest first) and ds_add_rtn on LDS counters give every key a bucket and a slot in it; an exclusive scan
+// turns counts into bucket bases; keys are scattered bucket-ordered and each key's rank is its bucket base
+// plus the number of larger keys in its own bucket.  Returns false, having written nothing into keys[0..K),
+// when the largest bucket holds more than `cap` keys (a skewed row): the caller ranks by full counting.
+template <int NSK>
+__device__ __forceinline__ bool bucket_rank(uint64_t* keys, uint32_t* base, const uint64_t (&sk)[NSK], int nsk, int K,
+                                            int lane, int cap) {
+    constexpr int NB = 256;
+    uint32_t hmin = 0xFFFFFFFFu, hmax = 0u;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        if (s < nsk && s * WAVE + lane < K) {
+            const uint32_t h = (uint32_t)(sk[s] >> 32);
+            hmin = min(hmin, h);
+            hmax = max(hmax, h);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        hmin = min(hmin, (uint32_t)__shfl_xor((int)hmin, off));
+        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+    }
+    // (float)(h - hmin) * scale is monotone in h and stays below 256 (two roundings of 255.99)
+    const float scale = hmax > hmin ? 255.99f / (float)(hmax - hmin) : 0.0f;
+    reinterpret_cast<uint4*>(base)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    if (lane == 0) base[NB] = 0u;
+    lds_fence();
+    uint32_t bk[NSK], slot[NSK];
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        bk[s] = 0u;
+        slot[s] = 0u;
+        if (s < nsk && s * WAVE + lane < K) {
+            const uint32_t d = min((uint32_t)((float)((uint32_t)(sk[s] >> 32) - hmin) * scale), (uint32_t)(NB - 1));
+            bk[s] = (uint32_t)(NB - 1) - d;
+            slot[s] = atomicAdd(&base[bk[s]], 1u);
+        }
+    }
+    lds_fence();
+    const uint4 c4 = reinterpret_cast<const uint4*>(base)[lane];
+    const uint32_t i1 = c4.x, i2 = i1 + c4.y, i3 = i2 + c4.z, i4 = i3 + c4.w;
+    uint32_t inc = i4;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
+        if (lane >= off) inc += y;
+    }
+    const uint32_t ex = inc - i4;
+    reinterpret_cast<uint4*>(base)[lane] = make_uint4(ex, ex + i1, ex + i2, ex + i3);
+    if (lane == 0) base[NB] = (uint32_t)K;
+    lds_fence();
+    uint32_t b0[NSK], b1[NSK];
+    uint32_t biggest = 0u;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        b0[s] = b1[s] = 0u;
+        if (s < nsk && s * WAVE + lane < K) {
+            b0[s] = base[bk[s]];
+            b1[s] = base[bk[s] + 1];
+            biggest = max(biggest, b1[s] - b0[s]);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) biggest = max(biggest, (uint32_t)__shfl_xor((int)biggest, off));
+    if (biggest > (uint32_t)cap) {
+        note_slow(base, lane);
+        return false;
+    }
+#pragma unroll
+    for (int s = 0; s < NSK; ++s)
+        if (b1[s] > b0[s]) keys[b0[s] + slot[s]] = sk[s];
+    lds_fence();
+    uint32_t rk[NSK];
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) rk[s] = b0[s];
+    for (uint32_t t = 0; t < biggest; ++t) {
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            const uint32_t idx = b0[s] + t;
+            if (idx < b1[s]) rk[s] += keys[idx] > sk[s] ? 1u : 0u;
+        }
+    }
+    lds_fence();
+#pragma unroll
+    for (int s = 0; s < NSK; ++s)
+        if (b1[s] > b0[s]) keys[rk[s]] = sk[s];
+    lds_fence();
+    return true;
+}
+
 // -inf for ids >= V (last tile only) and for banned ids (sorted; `bi`/`next_ban` advance monotonically)
 template <int W>
 __device__ __forceinline__ void mask_tile(const StepParams& p, float (&x)[W], int tile, int ntiles, int j0,
@@ -213,6 +420,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     constexpr int TS = WAVE * W;  // elements per tile (one 16-byte load per lane)
     static_assert(NSK * WAVE <= CAND - TS, "K must leave room for one tile of appends");
     __shared__ uint64_t s_keys[WPB][CAND];
+    __shared__ __attribute__((aligned(16))) uint32_t s_scr[WPB][SCR_U32];
 
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -241,6 +449,8 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     Cand cand;
     cand.keys = s_keys[wv];
+    cand.scr = s_scr[wv];
+    if (lane == 0) cand.scr[SCR_SLOW] = 0u;
     cand.cnt = 0;
     cand.ncompact = 0;
     cand.thr = -__builtin_inff();
@@ -367,7 +577,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     // ---------------- exact top-K, ranked ----------------
     uint64_t* keys = cand.keys;
-    if (cand.cnt > K) compact_topk(keys, cand.cnt, K, lane);
+    if (cand.cnt > K) compact_topk(keys, cand.scr, cand.cnt, K, lane);
     const int nsk = (K + WAVE - 1) / WAVE;
     const int K8 = (K + 7) & ~7;
     if (lane < K8 - K) keys[K + lane] = 0ull;  // zero pad: never counted as greater
@@ -380,22 +590,24 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         sk[s] = (s < nsk && i < K) ? keys[i] : 0ull;
         rk[s] = 0;
     }
-    for (int t = 0; t < K8; t += 8) {
-        uint64_t o[8];
+    if (!bucket_rank<NSK>(keys, cand.scr, sk, nsk, K, lane, NSG_BUCKET_CAP)) {
+        for (int t = 0; t < K8; t += 8) {  // skewed row: rank by counting (one LDS broadcast per key)
+            uint64_t o[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = keys[t + u];  // LDS broadcast reads, 8 in flight
+            for (int u = 0; u < 8; ++u) o[u] = keys[t + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 8; ++u)
 #pragma unroll
-            for (int s = 0; s < NSK; ++s) rk[s] += (o[u] > sk[s]) ? 1 : 0;
+                for (int s = 0; s < NSK; ++s) rk[s] += (o[u] > sk[s]) ? 1 : 0;
+        }
+        lds_fence();
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            const int i = s * WAVE + lane;
+            if (s < nsk && i < K) keys[rk[s]] = sk[s];
+        }
+        lds_fence();
     }
-    lds_fence();
-#pragma unroll
-    for (int s = 0; s < NSK; ++s) {
-        const int i = s * WAVE + lane;
-        if (s < nsk && i < K) keys[rk[s]] = sk[s];
-    }
-    lds_fence();
 #pragma unroll
     for (int s = 0; s < NSK; ++s) {
         const int i = s * WAVE + lane;
@@ -624,11 +836,14 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     }
     // rare-event diagnostics only (no per-step atomics): sharded by block so waves never contend
     const int overflow = cand.ncompact;
-    if (lane == 0 && p.counters && (exact || overflow > 0 || nfallback)) {
+    lds_fence();
+    const uint32_t nslow = cand.scr[SCR_SLOW];
+    if (lane == 0 && p.counters && (exact || overflow > 0 || nfallback || nslow)) {
         unsigned long long* c = p.counters + 4 * (blockIdx.x & (NS_COUNTER_SHARDS - 1));
         if (exact) atomicAdd(&c[0], 1ull);
         if (overflow > 0) atomicAdd(&c[1], (unsigned long long)overflow);
         if (nfallback) atomicAdd(&c[2], (unsigned long long)nfallback);
+        if (nslow) atomicAdd(&c[3], (unsigned long long)nslow);
     }
 }
 

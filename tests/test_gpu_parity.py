@@ -231,11 +231,13 @@ def _sample_ids(V, W=4):
     return np.asarray(ids)
 
 
-@pytest.mark.parametrize("mode", ["miss", "overflow"])
+@pytest.mark.parametrize("mode", ["miss", "overflow", "ties", "outlier"])
 def test_adversarial_rows_exercise_fallback_paths(mode):
     """Rows whose stratified sample is unrepresentative: 'miss' makes the speculative threshold too high
-    (the wave must re-read its row), 'overflow' makes it far too low (many compactions).  Tokens must
-    still match the oracle exactly."""
+    (the wave must re-read its row), 'overflow' makes it far too low (many compactions).  'ties' quantises
+    the logits to a few values (the histogram select falls back to bisection and the bucket rank to full
+    counting); 'outlier' puts one huge logit in the row every other step (all other keys crowd into one
+    bucket).  Tokens must still match the oracle exactly."""
     from neuralsteganography_amd.coder import CoderParams, EncodeSession, row_stride
 
     torch = _torch()
@@ -249,8 +251,12 @@ def test_adversarial_rows_exercise_fallback_paths(mode):
         x = synthetic.logits_row(77, s, t, V, 1.0)
         if mode == "miss":
             x[samp] += 12.0
-        else:
+        elif mode == "overflow":
             x[samp] -= 12.0
+        elif mode == "ties":
+            x = np.round(x * 2.0) / 2.0
+        elif t % 2 == 0:
+            x[(97 * t + 13 * s) % (V - 2)] = 3.0e30
         return x.astype(np.float32)
 
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 8)) for s in range(B)]
@@ -267,5 +273,7 @@ def test_adversarial_rows_exercise_fallback_paths(mode):
     assert sess.tokens() == expect
     if mode == "miss":
         assert c1[2] > c0[2], "speculation miss path was not exercised"
-    else:
+    elif mode == "overflow":
         assert c1[1] > c0[1], "overflow compaction path was not exercised"
+    else:
+        assert c1[3] > c0[3], "slow top-K selection path was not exercised"
