@@ -1061,16 +1061,29 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     p.nbanned = nb;
     for (int i = 0; i < nb; ++i) p.banned[i] = ban[i];
     p.flags = flags;
-    // speculative candidate threshold: the spec_j-th largest of a 1024-id stratified sample, chosen so that
-    // about 3.2*K ids of the row pass it (a guess verified per row; a miss costs one extra row read)
+    // speculative candidate threshold: the spec_j-th largest of a 1024-id stratified sample.  The number of
+    // sample ids above the row's true K-th key is ~Poisson(lambda = 1024 K / nvalid); spec_j is the smallest j
+    // with P(Poisson(lambda) >= j) <= 1e-6, so a miss (one extra row read by that wave) stays a rare event
+    // for every K.  NSG_SPEC_FACTOR (tuning override) instead sets spec_j = factor * lambda + 1.
     p.spec_j = 0;
-    static const double spec_factor = [] {  // tuning override (tools/): expected passes = factor * K
+    static const double spec_factor = [] {
         const char* e = getenv("NSG_SPEC_FACTOR");
-        return e ? atof(e) : 3.2;
+        return e ? atof(e) : 0.0;
     }();
-    if (ctx->vocab >= 2048 && spec_factor > 0.0) {
-        const double j = spec_factor * (double)K * 1024.0 / (double)nvalid;
-        int sj = (int)j + 1;
+    if (ctx->vocab >= 2048) {
+        const double lambda = (double)K * 1024.0 / (double)nvalid;
+        int sj;
+        if (spec_factor > 0.0) {
+            sj = (int)(spec_factor * lambda) + 1;
+        } else {
+            double term = exp(-lambda), tail = 1.0;  // tail = P(X >= j), term = P(X = j)
+            sj = 0;
+            while (tail > 1e-6 && sj < 1024) {
+                tail -= term;
+                ++sj;
+                term *= lambda / (double)sj;
+            }
+        }
         if (sj < 4) sj = 4;
         if (sj < 256) p.spec_j = sj;
     }

@@ -19,7 +19,10 @@ namespace nsg {
 #define NSG_CAND 1024
 #endif
 #ifndef NSG_PREFETCH
-#define NSG_PREFETCH 8
+#define NSG_PREFETCH 4
+#endif
+#ifndef NSG_LOAD_AUX
+#define NSG_LOAD_AUX 2  // cache policy of the streamed logit loads: nt (read-once stream)
 #endif
 #ifndef NSG_MIN_WAVES_PER_EU
 #define NSG_MIN_WAVES_PER_EU 4
@@ -214,7 +217,7 @@ struct RowReader {
         : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), (short)0,
                                                (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000)) {}
     __device__ __forceinline__ uint4 vec(int v) const {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, 0);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, NSG_LOAD_AUX);
         return make_uint4(r[0], r[1], r[2], r[3]);
     }
 };
