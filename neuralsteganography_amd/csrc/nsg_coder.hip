@@ -211,13 +211,29 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, uint32_t* scr, int
 
 // buffer-resource row reader: one SRD per wave (uniform), range-checked 16-byte loads (0 beyond the row)
 // Candidate buffer of one wave: keys of every element > thr seen so far (a superset of the running top-K).
+// Appends store raw entries (value bits << 32 | id: no order transform on the streaming path); entries
+// [0, conv) are canonical keys, [conv, cnt) raw, and to_keys() converts the raw tail before any read.
 struct Cand {
     uint64_t* keys;
     uint32_t* scr;  // per-wave LDS scratch (SCR_U32)
     int cnt;
+    int conv;
     int ncompact;
     float thr;  // element passes iff x > thr
 };
+
+__device__ __forceinline__ uint64_t raw_entry(float x, uint32_t j) {
+    return ((uint64_t)__float_as_uint(x) << 32) | (uint64_t)j;
+}
+
+__device__ __forceinline__ void to_keys(Cand& c, int lane) {
+    for (int i = c.conv + lane; i < c.cnt; i += WAVE) {
+        const uint64_t r = c.keys[i];
+        c.keys[i] = make_key(__uint_as_float((uint32_t)(r >> 32)), (uint32_t)r);
+    }
+    c.conv = c.cnt;
+    lds_fence();
+}
 
 template <int W>
 __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int K, int lane) {
@@ -233,9 +249,10 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
         npt += popc64(msk[q]);
     }
     if (c.cnt + npt > CAND) {  // cnt > CAND - TS >= K: keep the exact running top-K
+        to_keys(c, lane);
         const uint64_t kappa = compact_topk(c.keys, c.scr, c.cnt, K, lane);
         ++c.ncompact;
-        c.cnt = K;
+        c.cnt = c.conv = K;
         // later elements have larger ids than every buffered key, so ties at the K-th value rank below it
         c.thr = key_val(kappa);
         npt = 0;
@@ -248,7 +265,7 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
     int base = c.cnt;
 #pragma unroll
     for (int q = 0; q < W; ++q) {
-        if (x[q] > c.thr) c.keys[base + lanes_below(msk[q])] = make_key(x[q], (uint32_t)(j0 + q));
+        if (x[q] > c.thr) c.keys[base + lanes_below(msk[q])] = raw_entry(x[q], (uint32_t)(j0 + q));
         base += popc64(msk[q]);
     }
     c.cnt = base;
@@ -272,12 +289,6 @@ __device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
 template <int W, int G>
 __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int jb, int K, int lane) {
     constexpr int TS = WAVE * W;
-    float mx = x[0][0];
-#pragma unroll
-    for (int d = 0; d < G; ++d)
-#pragma unroll
-        for (int q = 0; q < W; ++q) mx = fmaxf(mx, x[d][q]);
-    if (!ballot(mx > c.thr)) return;
     int n = 0;
 #pragma unroll
     for (int d = 0; d < G; ++d)
@@ -285,6 +296,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
         for (int q = 0; q < W; ++q) n += (x[d][q] > c.thr) ? 1 : 0;
     int excl, total;
     wave_excl_prefix(n, excl, total);
+    if (total == 0) return;
     if (c.cnt + total > CAND) {
 #pragma unroll
         for (int d = 0; d < G; ++d) offer<W>(c, x[d], jb + d * TS, K, lane);
@@ -296,7 +308,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
 #pragma unroll
         for (int q = 0; q < W; ++q)
             if (x[d][q] > c.thr) {
-                c.keys[pos] = make_key(x[d][q], (uint32_t)(jb + d * TS + q));
+                c.keys[pos] = raw_entry(x[d][q], (uint32_t)(jb + d * TS + q));
                 ++pos;
             }
     c.cnt += total;
@@ -452,6 +464,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     cand.scr = s_scr[wv];
     if (lane == 0) cand.scr[SCR_SLOW] = 0u;
     cand.cnt = 0;
+    cand.conv = 0;
     cand.ncompact = 0;
     cand.thr = -__builtin_inff();
     int nfallback = 0;
@@ -558,6 +571,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     if (spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) {
         ++nfallback;
         cand.cnt = 0;
+        cand.conv = 0;
         cand.thr = -__builtin_inff();
         int bj = 0, nbj = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
         for (int tile = 0; tile < ntiles; ++tile) {
@@ -577,6 +591,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     // ---------------- exact top-K, ranked ----------------
     uint64_t* keys = cand.keys;
+    to_keys(cand, lane);
     if (cand.cnt > K) compact_topk(keys, cand.scr, cand.cnt, K, lane);
     const int nsk = (K + WAVE - 1) / WAVE;
     const int K8 = (K + 7) & ~7;
