@@ -68,6 +68,17 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(OrTrace)]
         L.or_row_sum.restype = ctypes.c_double
         L.or_row_sum.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.or_encode_step_stats.restype = ctypes.c_int
+        L.or_encode_step_stats.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                           ctypes.c_int, u8p, ctypes.c_int64, ctypes.POINTER(OrState), i32p,
+                                           ctypes.POINTER(OrTrace), dp]
+        L.or_rand64.restype = ctypes.c_uint64
+        L.or_rand64.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64]
+        L.or_sample_step.restype = ctypes.c_int
+        L.or_sample_step.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                     ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(OrState), i32p,
+                                     ctypes.POINTER(OrTrace), dp]
         L.or_encode_batch.restype = ctypes.c_int
         L.or_encode_batch.argtypes = [fp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, i32p, ctypes.c_int,
                                       ctypes.c_double, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int64,
@@ -105,7 +116,9 @@ def new_state(precision: int) -> OrState:
 
 
 def encode_step(row: np.ndarray, st: OrState, payload: np.ndarray, nbits: int, *, banned, temp: float,
-                precision: int, topk: int) -> Tuple[int, int, OrTrace]:
+                precision: int, topk: int, stats: np.ndarray = None) -> Tuple[int, int, OrTrace]:
+    """One encode step; ``stats`` (float64[4], optional) accumulates (sum log p(sel), sum KL bits,
+    sum entropy bits, steps) as code_base/arithmetic.py:193-199 defines them."""
     x = np.ascontiguousarray(row, dtype=np.float32)
     b = np.ascontiguousarray(banned, dtype=np.int32)
     pl = np.ascontiguousarray(payload, dtype=np.uint8)
@@ -113,8 +126,13 @@ def encode_step(row: np.ndarray, st: OrState, payload: np.ndarray, nbits: int, *
         pl = np.zeros(1, np.uint8)
     tok = ctypes.c_int32(-1)
     tr = OrTrace()
-    rc = lib().or_encode_step(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(precision), int(topk),
-                              _u8(pl), int(nbits), ctypes.byref(st), ctypes.byref(tok), ctypes.byref(tr))
+    if stats is None:
+        rc = lib().or_encode_step(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(precision), int(topk),
+                                  _u8(pl), int(nbits), ctypes.byref(st), ctypes.byref(tok), ctypes.byref(tr))
+    else:
+        rc = lib().or_encode_step_stats(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(precision),
+                                        int(topk), _u8(pl), int(nbits), ctypes.byref(st), ctypes.byref(tok),
+                                        ctypes.byref(tr), stats.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return rc, tok.value, tr
 
 
@@ -131,8 +149,17 @@ def decode_step(row: np.ndarray, st: OrState, token: int, is_last: bool, out_bit
 RowFn = Callable[[int], np.ndarray]
 
 
+def stats_summary(acc: np.ndarray, bits_consumed: int = None) -> dict:
+    """(sum log p, sum KL, sum H, n) -> the reference's averages (arithmetic.py:212-215, sample.py:50-52)."""
+    n = acc[3]
+    out = {"avg_NLL": -acc[0] / n, "avg_KL": acc[1] / n, "avg_Hq": acc[2] / n}
+    if bits_consumed is not None:
+        out["words_per_bit"] = n / bits_consumed
+    return out
+
+
 def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, precision: int, topk: int,
-                  max_steps: int = 1 << 20, sent_end=None) -> Tuple[List[int], List[OrTrace]]:
+                  max_steps: int = 1 << 20, sent_end=None, stats: np.ndarray = None) -> Tuple[List[int], List[OrTrace]]:
     """Encode one bit list (``code_base/arithmetic.py:112-210`` loop); ``row_fn(t)`` gives step t's logits.
 
     ``sent_end`` (a per-id boolean table) enables finish_sent (``:114,134-137``): after the payload, the
@@ -146,7 +173,7 @@ def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, pr
         if t >= max_steps:
             raise RuntimeError("oracle encode did not terminate")
         rc, tok, tr = encode_step(row_fn(t), st, packed, nbits, banned=banned, temp=temp, precision=precision,
-                                  topk=topk)
+                                  topk=topk, stats=stats)
         if rc != OR_OK:
             raise RuntimeError(f"oracle encode step {t} failed rc={rc}")
         toks.append(tok)
@@ -165,6 +192,75 @@ def encode_stream(row_fn: RowFn, bits: Sequence[int], *, banned, temp: float, pr
             if sent_end[tok]:
                 break
     return toks, traces
+
+
+def encode_bits_consumed(row_fn: RowFn, bits: Sequence[int], **kw) -> int:
+    """bit_pos after encoding ``bits`` (the reference's final ``i``, arithmetic.py:215)."""
+    nbits = len(bits)
+    packed = np.packbits(np.asarray(bits, dtype=np.uint8), bitorder="little") if nbits else np.zeros(1, np.uint8)
+    st = new_state(kw["precision"])
+    t = 0
+    while st.bit_pos < nbits:
+        rc, _, _ = encode_step(row_fn(t), st, packed, nbits, **kw)
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle encode step {t} failed rc={rc}")
+        t += 1
+    return int(st.bit_pos)
+
+
+def rand64(seed: int, gid: int, t: int) -> int:
+    return int(lib().or_rand64(int(seed) & ((1 << 64) - 1), int(gid), int(t)))
+
+
+def sample_step(row: np.ndarray, st: OrState, *, banned, temp: float, topk: int, seed: int, gid: int,
+                stats: np.ndarray = None) -> Tuple[int, OrTrace]:
+    x = np.ascontiguousarray(row, dtype=np.float32)
+    b = np.ascontiguousarray(banned, dtype=np.int32)
+    tok = ctypes.c_int32(-1)
+    tr = OrTrace()
+    sp = stats.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if stats is not None else None
+    rc = lib().or_sample_step(_fptr(x), x.size, _i32(b), b.size, 1.0 / float(temp), int(topk),
+                              int(seed) & ((1 << 64) - 1), int(gid), ctypes.byref(st), ctypes.byref(tok),
+                              ctypes.byref(tr), sp)
+    if rc != OR_OK:
+        raise RuntimeError(f"oracle sample step failed rc={rc}")
+    return tok.value, tr
+
+
+def sample_stream(row_fn: RowFn, length: int, *, banned, temp: float, topk: int, seed: int, gid: int,
+                  stats: np.ndarray = None) -> Tuple[List[int], List[OrTrace]]:
+    """``length`` canonical sampler steps (code_base/sample.py:22-48 loop); ``row_fn(t)`` gives step t's logits."""
+    st = new_state(1)
+    toks, traces = [], []
+    for t in range(length):
+        tok, tr = sample_step(row_fn(t), st, banned=banned, temp=temp, topk=topk, seed=seed, gid=gid, stats=stats)
+        toks.append(tok)
+        traces.append(tr)
+    return toks, traces
+
+
+def sample_stats_for_tokens(row_fn: RowFn, tokens: Sequence[int], *, banned, temp: float, topk: int) -> dict:
+    """The reference sampler's statistics (sample.py:31-48) for a GIVEN token sequence (e.g. the one torch
+    sampled): KL and entropy depend only on the rows, NLL on the tokens."""
+    acc = np.zeros(4)
+    for t, tok in enumerate(tokens):
+        x = np.asarray(row_fn(t), dtype=np.float64).copy()
+        valid = np.ones(x.size, bool)
+        valid[list(banned)] = False
+        m = x[valid].max()
+        lse1 = np.log(np.exp(x[valid] - m).sum())
+        order = np.lexsort((np.arange(x.size), -x))
+        order = order[valid[order]]
+        K = order.size if topk <= 0 else min(topk, order.size)
+        top = x[order[:K]] - m
+        z = top / temp
+        lq = z - np.log(np.exp(z).sum())
+        q = np.exp(lq)
+        acc[0] += (x[tok] - m) - lse1
+        acc[1] += np.sum(np.where(q > 0, q * (lq - (top - lse1)), 0.0)) / 0.69315
+        acc[2] += -np.sum(np.where(q > 0, q * lq, 0.0)) / 0.69315
+        acc[3] += 1
+    return stats_summary(acc)
 
 
 def decode_stream(row_fn: RowFn, tokens: Sequence[int], *, banned, temp: float, precision: int,

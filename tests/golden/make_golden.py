@@ -126,6 +126,26 @@ CONFIGS = {
 
 LOGIT_SEED = 7
 
+# code_base/sample.py (the non-stego token loop): name -> vocab, dtype, logit scale, temp, topk, token counts
+# per stream.  torch.multinomial draws from torch's seeded CPU generator (SAMPLE_TORCH_SEED).  The reference's
+# default topk=-1 cannot run: sample.py:39 slices base_log_probs[:-1] (V-1 entries) against V probabilities.
+SAMPLE_CONFIGS = {
+    "s1_v50257_f32_k300_t09": dict(vocab=50257, dtype="f32", scale=3.0, temp=0.9, topk=300, lengths=[64, 32]),
+    "s2_v50257_f32_k50000_t10": dict(vocab=50257, dtype="f32", scale=3.0, temp=1.0, topk=50000, lengths=[48]),
+    "s3_v50257_f16_k100_t09": dict(vocab=50257, dtype="f16", scale=3.0, temp=0.9, topk=100, lengths=[48]),
+    "s4_v700_f32_k690_t07": dict(vocab=700, dtype="f32", scale=2.0, temp=0.7, topk=690, lengths=[64]),
+}
+SAMPLE_TORCH_SEED = 1234
+
+
+class SampleModel(SyntheticModel):
+    """sample.py:26 calls ``logits, past = model(prev.unsqueeze(0), past=past)`` (the pre-transformers-5 tuple
+    API): return ``(logits, ())`` so ``limit_past`` (code_base/utils.py:19) sees an empty cache."""
+
+    def __call__(self, input_ids, past=None):
+        out = SyntheticModel.__call__(self, input_ids)
+        return out.logits, ()
+
 
 def run_config(name, cfg, ref, stable_sort_mode):
     dtype = np.float16 if cfg["dtype"] == "f16" else np.float32
@@ -162,8 +182,42 @@ def run_config(name, cfg, ref, stable_sort_mode):
     return out
 
 
+def run_sample_config(name, cfg, stable_sort_mode):
+    import torch
+
+    sys.path.insert(0, str(REF / "code_base"))
+    import sample as ref_sample  # code_base/sample.py
+
+    assert Path(ref_sample.__file__).resolve() == (REF / "code_base" / "sample.py").resolve()
+    dtype = np.float16 if cfg["dtype"] == "f16" else np.float32
+    out = {"tokens": [], "tok_off": [0], "stats": []}
+    torch.manual_seed(SAMPLE_TORCH_SEED)
+    for s, length in enumerate(cfg["lengths"]):
+        model = SampleModel(LOGIT_SEED, s, cfg["vocab"], cfg["scale"], dtype)
+        with stable_sort_mode():
+            toks, nll, kl_, hq = ref_sample.sample(model, StubTokenizer(), length, synthetic.DEFAULT_CONTEXT,
+                                                   temperature=cfg["temp"], device="cpu", topk=cfg["topk"])
+        assert len(toks) == length == model.calls
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["stats"].append([nll, kl_, hq])
+        print(f"  {name} s={s} length={length} NLL={nll:.4f} KL={kl_:.4f} Hq={hq:.4f}", flush=True)
+    return out
+
+
 def main(names=None):
     ref, stable = _import_reference()
+    for name, cfg in SAMPLE_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_sample_config(name, cfg, stable)
+        meta = dict(cfg, name=name, kind="sample", logit_seed=LOGIT_SEED, torch_seed=SAMPLE_TORCH_SEED,
+                    context=synthetic.DEFAULT_CONTEXT, banned=[cfg["vocab"] - 1, 628],
+                    reference="code_base/sample.py sample", sort="stable (value desc, id asc)")
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            stats=np.asarray(res["stats"], dtype=np.float64))
     for name, cfg in CONFIGS.items():
         if names and name not in names:
             continue

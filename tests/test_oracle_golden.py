@@ -56,3 +56,78 @@ def test_golden_fixtures_cover_the_configs():
     assert g.meta["precision"] == 26 and g.meta["topk"] == 300 and g.meta["temp"] == 0.9
     # ragged payload lengths including 1 bit
     assert sorted(len(s.msg) for s in g.streams)[0] == 1
+
+
+@pytest.mark.parametrize("name", [n for n in golden.names() if not n.endswith("_finish")])
+def test_oracle_encode_stats_match_reference(name):
+    """avg_NLL, avg_KL, words_per_bit, avg_Hq of code_base/arithmetic.py:193-215 (the stats the reference
+    returns with the tokens); the oracle restates them in float64 -> agreement to ~1e-12 relative."""
+    g = golden.load(name)
+    m = g.meta
+    for s in g.streams[:3]:
+        row = lambda t, s=s: g.row(s.stream, t).astype(np.float32)
+        acc = np.zeros(4)
+        kw = dict(banned=m["banned"], temp=m["temp"], precision=m["precision"], topk=m["topk"])
+        oracle.encode_stream(row, s.msg, stats=acc, **kw)
+        got = oracle.stats_summary(acc, oracle.encode_bits_consumed(row, s.msg, **kw))
+        ref = dict(zip(["avg_NLL", "avg_KL", "words_per_bit", "avg_Hq"], s.stats))
+        for k, v in ref.items():
+            assert got[k] == pytest.approx(v, rel=1e-9, abs=1e-12), (name, s.stream, k)
+
+
+@pytest.mark.parametrize("name", golden.sample_names())
+def test_oracle_sample_stats_match_reference(name):
+    """code_base/sample.py statistics recomputed for the tokens torch drew in the reference run.  The
+    reference evaluates them in the logits' dtype (sample.py:31-35 never calls .double()): rel 1e-5 for
+    float32 rows, 1e-3 for float16 rows (log_softmax output rounded to half precision)."""
+    g = golden.load_sample(name)
+    m = g.meta
+    for s in g.streams:
+        row = lambda t, s=s: g.row(s.stream, t).astype(np.float32)
+        got = oracle.sample_stats_for_tokens(row, s.tokens, banned=m["banned"], temp=m["temp"], topk=m["topk"])
+        rel = 1e-3 if m["dtype"] == "f16" else 1e-5
+        for k, v in zip(["avg_NLL", "avg_KL", "avg_Hq"], s.stats):
+            assert got[k] == pytest.approx(v, rel=rel, abs=rel / 10), (name, s.stream, k)
+
+
+@pytest.mark.parametrize("name", golden.sample_names())
+def test_oracle_sampler_canonical_step(name):
+    """The canonical sampler (oracle C): every draw lies in the reference's top-k set, and its KL / entropy
+    (which depend on the rows only) equal the reference run's; NLL is consistent with its own draws."""
+    g = golden.load_sample(name)
+    m = g.meta
+    s = g.streams[0]
+    row = lambda t: g.row(s.stream, t).astype(np.float32)
+    acc = np.zeros(4)
+    toks, _ = oracle.sample_stream(row, len(s.tokens), banned=m["banned"], temp=m["temp"], topk=m["topk"],
+                                   seed=99, gid=s.stream, stats=acc)
+    got = oracle.stats_summary(acc)
+    rel = 1e-3 if m["dtype"] == "f16" else 1e-5  # the reference computes in the logits' dtype
+    assert got["avg_KL"] == pytest.approx(s.stats[1], rel=rel, abs=rel / 10)
+    assert got["avg_Hq"] == pytest.approx(s.stats[2], rel=rel, abs=rel / 10)
+    mine = oracle.sample_stats_for_tokens(row, toks, banned=m["banned"], temp=m["temp"], topk=m["topk"])
+    assert got["avg_NLL"] == pytest.approx(mine["avg_NLL"], rel=1e-9)
+    for t, tok in enumerate(toks):
+        x = row(t).astype(np.float64)
+        x[m["banned"]] = -np.inf
+        order = np.lexsort((np.arange(x.size), -x))
+        assert tok in set(order[: m["topk"]].tolist())
+
+
+def test_oracle_sampler_distribution():
+    """Frequencies of the canonical sampler over many counter-based draws match softmax(x/T) over the top-k
+    (chi-square, 2000 draws on a 12-id row)."""
+    x = np.array([2.0, 1.5, 1.5, 0.3, -0.2, 0.9, 1.1, -1.0, 0.0, 0.5, 2.2, -3.0], np.float32)
+    temp, topk, n = 0.8, 8, 2000
+    counts = np.zeros(x.size)
+    for g in range(n):
+        st = oracle.new_state(1)
+        tok, _ = oracle.sample_step(x, st, banned=[], temp=temp, topk=topk, seed=5, gid=g)
+        counts[tok] += 1
+    order = np.lexsort((np.arange(x.size), -x.astype(np.float64)))[:topk]
+    z = x[order].astype(np.float64) / temp
+    p = np.exp(z - z.max())
+    p /= p.sum()
+    assert counts.sum() == counts[order].sum()
+    chi2 = float(np.sum((counts[order] - n * p) ** 2 / (n * p)))
+    assert chi2 < 24.3, chi2  # 7 dof, p = 0.001
