@@ -124,6 +124,27 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
  * is_sent_finish).  The caller keeps it alive; NULL clears it. */
 int ns_set_sentence_end(ns_ctx* ctx, const uint8_t* d_table);
 
+/* Statistics of the encode steps (code_base/arithmetic.py:193-199, returned by encode_arithmetic :217):
+ * d_stats is a DEVICE array [B][4] of doubles that every later ns_encode_step accumulates into, per
+ * stream: [0] sum of log p(selected) under the untempered softmax, [1] sum of KL(q || p) in bits over the
+ * kept CDF entries, [2] sum of the tempered softmax's entropy over V in bits, [3] message-phase steps.
+ * avg_NLL = -[0]/[3], avg_KL = [1]/[3], avg_Hq = [2]/[3], words_per_bit = [3]/bit_pos.  Float64 values
+ * computed from fp32 streaming sums: within 1e-5 relative of the float64 reference (not bit-exact).
+ * NULL switches statistics off (the default, and the fast kernel). */
+int ns_set_stats(ns_ctx* ctx, double* d_stats);
+
+/* One sampler step (code_base/sample.py:22-48, the non-stego token loop) for streams [0,B): top-k of the
+ * banned-masked row (topk <= 0: every id, which the reference's sample.py:39 cannot run), temperature
+ * softmax, one draw.  The draw is counter based: u = splitmix64(seed, stream_offset + b, ntokens of the
+ * stream), the token is the first rank whose 2^48-scaled integer CDF exceeds (u * total) >> 64 -- bit-exact
+ * against oracle/nsg_oracle.c or_sample_step, and distributed as torch.multinomial (sample.py:44).
+ * d_state: only ntokens is used (set it to 0 with ns_init_state); d_stats: optional [B][4] as in
+ * ns_set_stats with [1] = KL(p_tau,k || p) and [2] = entropy of p_tau,k over the top-k set. */
+int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_t seed, int64_t stream_offset,
+                   ns_stream_state* d_state, int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride,
+                   double temp, int topk, const int32_t* banned, int nbanned, double* d_stats,
+                   ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
+
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
  * (row re-read), counters[3] = top-K selections that left the histogram fast path (value ties or a skewed

@@ -160,10 +160,29 @@ def _state_fields(state) -> dict:
             "ntokens": w32[:, 6], "flags": w32[:, 7].view(np.uint32)}
 
 
-class EncodeSession:
-    """B streams being encoded; call :meth:`step` once per generated token with that step's logits."""
+def _stats_rows(acc: np.ndarray, bits_consumed: Optional[np.ndarray] = None) -> List[dict]:
+    """[B, 4] accumulators (sum log p, sum KL bits, sum H bits, n) -> the reference's averages per stream
+    (``code_base/arithmetic.py:212-215``, ``sample.py:50-52``); NaN where a stream had no counted step."""
+    out = []
+    for i in range(acc.shape[0]):
+        n = acc[i, 3]
+        d = {"avg_NLL": -acc[i, 0] / n if n else math.nan, "avg_KL": acc[i, 1] / n if n else math.nan,
+             "avg_Hq": acc[i, 2] / n if n else math.nan}
+        if bits_consumed is not None:
+            d["words_per_bit"] = n / bits_consumed[i] if bits_consumed[i] else math.nan
+        out.append(d)
+    return out
 
-    def __init__(self, ctx: CoderContext, payload_bits: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+
+class EncodeSession:
+    """B streams being encoded; call :meth:`step` once per generated token with that step's logits.
+
+    ``stats=True`` also accumulates the statistics ``encode_arithmetic`` returns (avg_NLL, avg_KL,
+    words_per_bit, avg_Hq; ``code_base/arithmetic.py:193-217``) on the device -- within a float64
+    tolerance of the reference, not bit-exact -- at the cost of a heavier kernel build."""
+
+    def __init__(self, ctx: CoderContext, payload_bits: Sequence[Sequence[int]], max_tokens: Optional[int] = None,
+                 stats: bool = False):
         torch = _torch()
         self.ctx = ctx
         self.B = len(payload_bits)
@@ -186,11 +205,18 @@ class EncodeSession:
         self.hist = torch.full((self.B, cap), -1, dtype=torch.int32, device=dev)
         self.trace = None
         self.steps = 0
+        self.stats_acc = torch.zeros((self.B, 4), dtype=torch.float64, device=dev) if stats else None
 
     def enable_trace(self):
         torch = _torch()
         self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
         return self.trace
+
+    def stats(self) -> List[dict]:
+        """Per-stream avg_NLL, avg_KL, words_per_bit, avg_Hq (as ``encode_arithmetic`` returns them)."""
+        if self.stats_acc is None:
+            raise ConfigurationError("the session was created without stats=True")
+        return _stats_rows(self.stats_acc.cpu().numpy(), self.fields()["bit_pos"])
 
     def step(self, logits, *, force_exact: bool = False, finish_sent: bool = False, diag_flags: int = 0):
         """One coder step on ``logits`` ([B, ld] contiguous rows, ld = :func:`row_stride`).
@@ -203,11 +229,16 @@ class EncodeSession:
         flags = (_lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0) | int(diag_flags)
         if finish_sent:
             flags |= _lib.NS_STEP_FINISH_SENT
-        rc = _lib.lib().ns_encode_step(
+        L = _lib.lib()
+        if self.stats_acc is not None:
+            self.ctx.check(L.ns_set_stats(self.ctx._h, _ptr(self.stats_acc)), "ns_set_stats")
+        rc = L.ns_encode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
             _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), self.hist.shape[1],
             float(p.temp), int(p.topk), self.ctx._banned, self.ctx._nbanned, _ptr(self.trace), flags,
             _stream_handle())
+        if self.stats_acc is not None:
+            L.ns_set_stats(self.ctx._h, ctypes.c_void_p(0))
         self.ctx.check(rc, "ns_encode_step")
         self.steps += 1
         return self.out_token
@@ -322,10 +353,12 @@ class DecodeSession:
 
 
 def encode_batch(ctx: CoderContext, payload_bits: Sequence[Sequence[int]], logits_fn, *, max_steps: int = 1 << 20,
-                 check_every: int = 32, force_exact: bool = False, finish_sent: bool = False) -> List[List[int]]:
+                 check_every: int = 32, force_exact: bool = False, finish_sent: bool = False,
+                 return_stats: bool = False):
     """Run encode steps until every stream has consumed its payload; ``logits_fn(step, last_tokens)``
-    returns the ``[B, ld]`` logits of that step."""
-    sess = EncodeSession(ctx, payload_bits)
+    returns the ``[B, ld]`` logits of that step.  ``return_stats=True`` returns ``(tokens, stats)`` with the
+    per-stream statistics of ``encode_arithmetic`` (see :meth:`EncodeSession.stats`)."""
+    sess = EncodeSession(ctx, payload_bits, stats=return_stats)
     last = sess.out_token
     for t in range(max_steps):
         if t % check_every == 0:
@@ -335,6 +368,8 @@ def encode_batch(ctx: CoderContext, payload_bits: Sequence[Sequence[int]], logit
         last = sess.step(logits_fn(t, last), force_exact=force_exact, finish_sent=finish_sent)
     else:
         raise ConfigurationError("encode did not finish within max_steps")
+    if return_stats:
+        return sess.tokens(), sess.stats()
     return sess.tokens()
 
 
@@ -344,3 +379,77 @@ def decode_batch(ctx: CoderContext, token_lists: Sequence[Sequence[int]], logits
     for t in range(sess.T):
         sess.step(logits_fn(t, sess.tok[t]), force_exact=force_exact)
     return sess.bits()
+
+
+class SampleSession:
+    """B independent non-stego sampling streams (``code_base/sample.py:22-48``), one HIP launch per token.
+
+    Draws are counter based (``ns_sample_step``): token t of stream b uses splitmix64(seed, stream_offset + b,
+    t), so a run is reproducible and shardable (a rank passes its first global stream id as
+    ``stream_offset``).  ``topk <= 0`` samples from every id.  Statistics (avg_NLL, avg_KL, avg_Hq of
+    ``sample()``) are accumulated on the device when ``stats=True``."""
+
+    def __init__(self, ctx: CoderContext, B: int, *, seed: int, topk: int, temp: float, stream_offset: int = 0,
+                 max_tokens: int = 1024, stats: bool = True):
+        torch = _torch()
+        if B < 1 or B > ctx.max_batch:
+            raise ConfigurationError(f"batch {B} outside [1, {ctx.max_batch}]")
+        if not temp > 0:
+            raise ConfigurationError("temperature must be positive")
+        self.ctx, self.B = ctx, int(B)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.topk, self.temp, self.stream_offset = int(topk), float(temp), int(stream_offset)
+        dev = torch.device("cuda", ctx.device)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        self.out_token = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.hist = torch.full((self.B, int(max_tokens)), -1, dtype=torch.int32, device=dev)
+        self.stats_acc = torch.zeros((self.B, 4), dtype=torch.float64, device=dev) if stats else None
+        self.trace = None
+        self.steps = 0
+
+    def enable_trace(self):
+        torch = _torch()
+        self.trace = torch.zeros((self.B, 4), dtype=torch.int64, device=self.state.device)
+        return self.trace
+
+    def step(self, logits, *, diag_flags: int = 0):
+        p = self.ctx.params
+        if logits.dtype != p.torch_dtype or logits.dim() != 2 or logits.shape[0] != self.B or not logits.is_cuda:
+            raise ConfigurationError(f"logits must be [{self.B}, ld] {p.dtype} on the GPU")
+        if self.steps >= self.hist.shape[1]:
+            raise ConfigurationError("token history full: raise max_tokens")
+        rc = _lib.lib().ns_sample_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, ctypes.c_uint64(self.seed), self.stream_offset,
+            _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), self.hist.shape[1], self.temp, self.topk,
+            self.ctx._banned, self.ctx._nbanned, _ptr(self.stats_acc), _ptr(self.trace), int(diag_flags),
+            _stream_handle())
+        self.ctx.check(rc, "ns_sample_step")
+        self.steps += 1
+        return self.out_token
+
+    def trace_rows(self) -> np.ndarray:
+        t = self.trace.cpu().numpy().view(np.int32).reshape(self.B, 8)
+        return np.rec.fromarrays([t[:, 0], t[:, 1], t[:, 2], t[:, 3], t[:, 4]], names="k,kprime,sel,n,token")
+
+    def tokens(self) -> List[List[int]]:
+        h = self.hist.cpu().numpy()
+        n = min(self.steps, self.hist.shape[1])
+        return [h[i, :n].astype(np.int64).tolist() for i in range(self.B)]
+
+    def stats(self) -> List[dict]:
+        if self.stats_acc is None:
+            raise ConfigurationError("the session was created without stats=True")
+        return _stats_rows(self.stats_acc.cpu().numpy())
+
+
+def sample_batch(ctx: CoderContext, B: int, length: int, logits_fn, *, seed: int, topk: int, temp: float,
+                 stream_offset: int = 0, stats: bool = True):
+    """``length`` sampler steps for B streams; ``logits_fn(step, last_tokens)`` returns the ``[B, ld]``
+    logits.  Returns ``(tokens, stats)`` (stats None when ``stats=False``)."""
+    sess = SampleSession(ctx, B, seed=seed, topk=topk, temp=temp, stream_offset=stream_offset,
+                         max_tokens=max(1, length), stats=stats)
+    last = sess.out_token
+    for t in range(length):
+        last = sess.step(logits_fn(t, last))
+    return sess.tokens(), (sess.stats() if stats else None)

@@ -426,7 +426,98 @@ __device__ __forceinline__ void mask_tile(const StepParams& p, float (&x)[W], in
     }
 }
 
-template <typename T, bool DECODE, int NSK>
+// Sampler tail (code_base/sample.py:28-46; canonical steps S2-S5 of oracle/nsg_oracle.c): the ranked top-K
+// keys sk[] and their e_i are given.  Support k_s = leading ranks with e_i >= 2^-60; E canonical over it;
+// integer CDF at 2^48; counter-based draw; the interval state is not touched.
+template <int NSK>
+__device__ __forceinline__ void sample_tail(const StepParams& p, int b, const ns_stream_state& st,
+                                            const uint64_t (&sk)[NSK], const double (&e)[NSK], int nsk, int K,
+                                            double m, const RowStats& rs, int lane, bool stats) {
+    int ks = K;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        if (s < nsk) {
+            const int i = s * WAVE + lane;
+            const uint64_t mb = ballot(i < K && e[s] < SAMPLE_SUPPORT);
+            if (mb && ks == K) ks = s * WAVE + __builtin_ctzll(mb);
+        }
+    }
+    double el = 0.0;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s)
+        if (s < nsk && s * WAVE + lane < ks) el += e[s];
+    const double E = wave_sum_butterfly(el);
+    int64_t cum[NSK];
+    int64_t carry = 0;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        const int i = s * WAVE + lane;
+        const int64_t q = (s < nsk && i < ks) ? (int64_t)__builtin_rint((e[s] / E) * SAMPLE_SCALE) : 0;
+        const int64_t c = (s < nsk) ? wave_incl_scan(q, lane) + carry : carry;
+        cum[s] = c;
+        if (s < nsk) carry = __shfl(c, WAVE - 1);
+    }
+    const uint64_t total = (uint64_t)carry;
+    const uint64_t u = rand64(p.seed, p.stream_offset + b, st.ntokens);
+    const uint64_t idx = __umul64hi(u, total);
+    int sel = -1;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s) {
+        if (s < nsk) {
+            const int i = s * WAVE + lane;
+            const uint64_t ms = ballot(i < ks && (uint64_t)cum[s] > idx);
+            if (ms && sel < 0) sel = s * WAVE + __builtin_ctzll(ms);
+        }
+    }
+    uint64_t tk = 0;
+#pragma unroll
+    for (int s = 0; s < NSK; ++s)
+        if (s == sel / WAVE) tk = __shfl(sk[s], sel % WAVE);
+    const int32_t token = (int32_t)key_id(tk);
+    double kl = 0.0, h = 0.0;
+    if (stats) {
+        const double logE = log(E);
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            if (s < nsk && s * WAVE + lane < ks) {
+                const double xi = (double)key_val(sk[s]) - m;
+                const double lq = xi * p.inv_temp - logE;
+                const double q = e[s] / E;
+                kl += q * (lq - (xi - rs.lse1));
+                h += q * lq;
+            }
+        }
+        kl = wave_sum_butterfly(kl);
+        h = wave_sum_butterfly(h);
+    }
+    if (lane == 0) {
+        ns_stream_state ns = st;
+        ns.ntokens = st.ntokens + 1;
+        p.state[b] = ns;
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        if (p.trace) {
+            ns_step_trace tr;
+            tr.k = K;
+            tr.kprime = ks;
+            tr.sel = sel;
+            tr.n = 0;
+            tr.token = token;
+            tr.exact = 0;
+            tr.S = E;
+            p.trace[b] = tr;
+        }
+        if (stats) {
+            double* a = p.stats + 4 * (int64_t)b;
+            a[0] += ((double)key_val(tk) - m) - rs.lse1;
+            a[1] += kl / 0.69315;
+            a[2] += -h / 0.69315;
+            a[3] += 1.0;
+        }
+    }
+}
+
+template <typename T, bool DECODE, int NSK, bool STATS>
 __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_kernel(StepParams p) {
     constexpr int W = Elem<T>::W;
     constexpr int TS = WAVE * W;  // elements per tile (one 16-byte load per lane)
@@ -442,7 +533,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     ns_stream_state st = p.state[b];
     if (st.flags & NS_ST_DONE) return;
     int64_t nbits = 0;
-    if (!DECODE) {
+    if (!DECODE && !p.sample) {
         nbits = p.nbits[b];
         if (st.bit_pos >= nbits) {  // payload consumed: done, or sentence finishing (finish_sent_kernel)
             if (lane == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
@@ -509,6 +600,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     // ---------------- streaming pass (the HBM-bound part) ----------------
     double acc64 = 0.0;
+    double b64 = 0.0, u64 = 0.0;  // STATS: sum e (x-r), sum exp(x-r) untempered
     int bi = 0;
     int next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
     uint4 buf[PREFETCH];
@@ -525,13 +617,32 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         r = wave_max(mx);
         if (r == -__builtin_inff()) r = 0.0f;
     }
+    // fp32 partial sums of one group, flushed into float64 (STATS adds sum e*(x-r) and the untempered sum;
+    // masked ids are -inf: dx is clamped so e*dx is 0, not NaN)
+    auto accumulate = [&](const float* xs, int n) {
+        float a = 0.0f, bb = 0.0f, uu = 0.0f;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            if (STATS) {
+                const float dx = fmaxf(xs[i] - r, -3.0e38f);
+                const float e = __builtin_amdgcn_exp2f(dx * c32);
+                a += e;
+                bb += e * dx;
+                uu += __builtin_amdgcn_exp2f(dx * L2E_F);
+            } else {
+                a += __builtin_amdgcn_exp2f((xs[i] - r) * c32);
+            }
+        }
+        acc64 += (double)a;
+        if (STATS) {
+            b64 += (double)bb;
+            u64 += (double)uu;
+        }
+    };
     auto process = [&](float (&x)[W], int tile) {
         const int j0 = (tile * WAVE + lane) * W;
         mask_tile<W>(p, x, tile, ntiles, j0, bi, next_ban);
-        float a = 0.0f;
-#pragma unroll
-        for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((x[q] - r) * c32);
-        acc64 += (double)a;
+        accumulate(x, W);
         offer<W>(cand, x, j0, K, lane);
     };
     // Full groups: every slot is consumed, then refilled PREFETCH tiles ahead into the same registers
@@ -550,12 +661,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 #pragma unroll
             for (int d = 0; d < PREFETCH; ++d) mask_tile<W>(p, xg[d], tile + d, ntiles, jb + d * TS, bi, next_ban);
         }
-        float a = 0.0f;
-#pragma unroll
-        for (int d = 0; d < PREFETCH; ++d)
-#pragma unroll
-            for (int q = 0; q < W; ++q) a += __builtin_amdgcn_exp2f((xg[d][q] - r) * c32);
-        acc64 += (double)a;
+        accumulate(&xg[0][0], PREFETCH * W);
         offer_group<W, PREFETCH>(cand, xg, jb, K, lane);
     }
 #pragma unroll
@@ -642,12 +748,24 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         const int i = s * WAVE + lane;
         e[s] = (s < nsk && i < K) ? exp_canon(((double)key_val(sk[s]) - m) * p.inv_temp) : 0.0;
     }
+    const double S_r = wave_sum_butterfly(acc64);
+    // row statistics (STATS builds; tolerance-checked, not part of the bit contract)
+    RowStats rs{0.0, 0.0, 0.0};
+    const bool want_stats = STATS && p.stats != nullptr;
+    if (want_stats) {
+        const double B_r = wave_sum_butterfly(b64);
+        const double U_r = wave_sum_butterfly(u64);
+        if (!row_stats_from_stream(S_r, B_r, U_r, r, m, p.inv_temp, rs)) rs = wave_row_stats<T>(p, rowc, m, lane);
+    }
+    if (!DECODE && p.sample) {
+        sample_tail<NSK>(p, b, st, sk, e, nsk, K, m, rs, lane, want_stats);
+        return;
+    }
     const uint64_t R = st.hi - st.lo;
     const double Rd = (double)R;
     const double thr = 1.0 / Rd;
 
     // fast denominator with a rigorous interval
-    const double S_r = wave_sum_butterfly(acc64);
     const double t_m = (m - (double)r) * (double)c32;
     bool exact = (p.flags & NS_STEP_FORCE_EXACT_SUM) != 0u;
     exact = exact || !(S_r > 0.0 && S_r < 1.0e300) || !(t_m <= 100.0 && t_m >= -60.0);
@@ -776,13 +894,38 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         if (sel < 0) err = NS_ST_ERR_DIVERGE;
     }
 
+    uint64_t tk = 0;
     if (sel >= 0) {
-        uint64_t tk = 0;
         const int si = sel / WAVE, li = sel % WAVE;
 #pragma unroll
         for (int s = 0; s < NSK; ++s)
             if (s == si) tk = __shfl(sk[s], li);
         token = (int32_t)key_id(tk);
+    }
+
+    // statistics of an encode step (code_base/arithmetic.py:193-199): log p(sel) untempered, KL(q || p) over
+    // the k' kept entries with q = probs_final / R, entropy of the tempered softmax over V
+    if (!DECODE && want_stats && sel >= 0) {
+        const int64_t deficit = shift - (int64_t)st.lo;
+        double kl = 0.0;
+#pragma unroll
+        for (int s = 0; s < NSK; ++s) {
+            const int i = s * WAVE + lane;
+            if (s < nsk && i < kp) {
+                int64_t pf = (int64_t)__builtin_rint((e[s] / E) * Rd);
+                if (i == 0) pf += deficit;
+                const double qd = (double)pf / Rd;
+                if (qd > 0.0) kl += qd * (log(qd) - (((double)key_val(sk[s]) - m) - rs.lse1));
+            }
+        }
+        kl = wave_sum_butterfly(kl);
+        if (lane == 0) {
+            double* a = p.stats + 4 * (int64_t)b;
+            a[0] += ((double)key_val(tk) - m) - rs.lse1;
+            a[1] += kl / 0.69315;
+            a[2] += (rs.lst - rs.a_over_s) / 0.69315;
+            a[3] += 1.0;
+        }
     }
 
     // state update: cross-lane values are gathered by shuffles, every lane computes the same scalars
@@ -940,7 +1083,10 @@ static int fail(ns_ctx* ctx, int code, const std::string& msg) {
 template <typename T, bool DECODE, int NSK>
 static void launch_one(const nsg::StepParams& p, hipStream_t s) {
     const dim3 grid((p.B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
-    hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK>), grid, block, 0, s, p);
+    if (!DECODE && p.stats)  // statistics build (encode / sample only)
+        hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, !DECODE>), grid, block, 0, s, p);
+    else
+        hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, false>), grid, block, 0, s, p);
 }
 
 template <typename T, bool DECODE>
@@ -973,7 +1119,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.5 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.6 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -1006,6 +1152,7 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->d_counters = nullptr;
     ctx->wide = NsgWide();
     ctx->sent_end = nullptr;
+    ctx->stats = nullptr;
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
@@ -1125,6 +1272,7 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
     p.out_token = d_out_token;
     p.hist = d_token_hist;
     p.hist_stride = d_token_hist ? hist_stride : 0;
+    p.stats = ctx->stats;
     if (step_flags & NS_STEP_FINISH_SENT) {
         if (!ctx->sent_end) return fail(ctx, NS_ERR_CONFIG, "NS_STEP_FINISH_SENT needs ns_set_sentence_end");
         const dim3 g((B + nsg::WPB - 1) / nsg::WPB), blk(nsg::WPB * nsg::WAVE);
@@ -1156,6 +1304,35 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
     const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, true, (hipStream_t)hip_stream)
                                                   : launch<true>(ctx, p, (hipStream_t)hip_stream);
     if (!ok) return fail(ctx, NS_ERR_HIP, "ns_decode_step: launch failed");
+    return NS_OK;
+}
+
+int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_t seed, int64_t stream_offset,
+                   ns_stream_state* d_state, int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride,
+                   double temp, int topk, const int32_t* banned, int nbanned, double* d_stats,
+                   ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
+    nsg::StepParams p;
+    const int tk = topk > 0 ? topk : ctx->vocab;  // sample.py: topk <= 0 keeps every id
+    int rc = prepare(ctx, p, d_logits, ld, B, temp, tk, banned, nbanned, d_trace, step_flags, d_state);
+    if (rc != NS_OK) return rc;
+    if (!d_out_token) return fail(ctx, NS_ERR_CONFIG, "ns_sample_step: null output pointer");
+    p.sample = 1;
+    p.seed = seed;
+    p.stream_offset = stream_offset;
+    p.stats = d_stats;
+    p.out_token = d_out_token;
+    p.hist = d_token_hist;
+    p.hist_stride = d_token_hist ? hist_stride : 0;
+    const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, false, (hipStream_t)hip_stream)
+                                                  : launch<false>(ctx, p, (hipStream_t)hip_stream);
+    if (!ok) return fail(ctx, NS_ERR_HIP, "ns_sample_step: launch failed");
+    return NS_OK;
+}
+
+int ns_set_stats(ns_ctx* ctx, double* d_stats) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
+    ctx->stats = d_stats;
     return NS_OK;
 }
 

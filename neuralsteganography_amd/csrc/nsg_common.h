@@ -173,11 +173,49 @@ struct StepParams {
     const uint8_t* active;
     uint8_t* out_bits;
     int64_t out_stride;
+    // sampler (ns_sample_step): code_base/sample.py token loop
+    int sample;              // 1: sampler step (no interval, no payload)
+    uint64_t seed;           // counter-based draw: rand64(seed, stream_offset + b, ntokens)
+    int64_t stream_offset;
+    // statistics sink [B][4]: sum log p(sel), sum KL bits, sum entropy bits, steps (nullable)
+    double* stats;
     // common
     ns_stream_state* state;
     ns_step_trace* trace;
     unsigned long long* counters;
 };
+
+// counter-based 64-bit draw, identical to or_rand64 (oracle/nsg_oracle.c): splitmix64 finaliser
+__device__ __forceinline__ uint64_t rand64(uint64_t seed, int64_t gid, int64_t t) {
+    uint64_t z = seed ^ ((uint64_t)gid * 0xD1B54A32D192ED03ull);
+    z += (uint64_t)(t + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+constexpr float L2E_F = 1.44269504088896341f;   // log2(e), fp32 (untempered fast exps of the statistics)
+constexpr double SAMPLE_SUPPORT = 0x1p-60;       // sampler support: e_i >= 2^-60 (oracle step S2)
+constexpr double SAMPLE_SCALE = 0x1p48;          // sampler CDF resolution (oracle step S4)
+
+// Fast statistics of one row relative to its max m (tolerance-checked, not part of the bit contract):
+// lse1 = ln sum exp(x - m) (untempered), lst = ln sum exp((x - m)/T), a_over_s = sum p_T (x - m)/T.
+struct RowStats {
+    double lse1, lst, a_over_s;
+};
+
+// From the streaming accumulators taken against the reference r: S_r = sum 2^((x-r)c32), B_r = sum
+// 2^((x-r)c32) (x-r), U_r = sum 2^((x-r) log2 e).  Returns false when they are unusable (overflow).
+__device__ __forceinline__ bool row_stats_from_stream(double S_r, double B_r, double U_r, float r, double m,
+                                                      double inv_temp, RowStats& rs) {
+    if (!(S_r > 0.0 && S_r < 1.0e300 && U_r > 0.0 && U_r < 1.0e300 && B_r > -1.0e300 && B_r < 1.0e300))
+        return false;
+    const double rm = (double)r - m;
+    rs.lse1 = log(U_r) + rm;
+    rs.lst = log(S_r) + rm * inv_temp;
+    rs.a_over_s = inv_temp * (B_r / S_r + rm);
+    return true;
+}
 
 __device__ __forceinline__ bool is_banned(const StepParams& p, int j) {
     bool b = false;
@@ -202,6 +240,28 @@ __device__ __forceinline__ double exact_row_sum(const StepParams& p, const void*
         }
     }
     return wave_sum_butterfly(acc);
+}
+
+// Statistics fallback (streaming accumulators unusable): re-read the row, float64 exps against the true max.
+template <typename T>
+__device__ __noinline__ RowStats wave_row_stats(const StepParams& p, const void* row, double m, int lane) {
+    double s1 = 0.0, st = 0.0, at = 0.0;
+    for (int j = lane; j < p.V; j += WAVE) {
+        if (is_banned(p, j)) continue;
+        const double d = (double)(Elem<T>::load1(row, j) + 0.0f) - m;
+        const double et = exp(d * p.inv_temp);
+        s1 += exp(d);
+        st += et;
+        at += et * (d * p.inv_temp);
+    }
+    s1 = wave_sum_butterfly(s1);
+    st = wave_sum_butterfly(st);
+    at = wave_sum_butterfly(at);
+    RowStats rs;
+    rs.lse1 = log(s1);
+    rs.lst = log(st);
+    rs.a_over_s = at / st;
+    return rs;
 }
 
 __device__ __forceinline__ const void* uniform_ptr(const void* ptr) {

@@ -21,6 +21,7 @@ struct WideStat {
     double S_fast;
     uint32_t exact;   // 1: the fast bound is unusable, the CDF kernel computes the exact sum
     uint32_t pad;
+    double S_r, B_r, U_r;  // raw streaming sums against r (statistics: row_stats_from_stream)
 };
 
 }  // namespace nsg
@@ -47,6 +48,7 @@ struct ns_ctx {
     unsigned long long* d_counters;
     NsgWide wide;
     const uint8_t* sent_end;  // device table [vocab] for NS_STEP_FINISH_SENT (ns_set_sentence_end)
+    double* stats;            // encode statistics sink [B][4] (ns_set_stats), nullable
     std::string err;
 };
 

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
     if (b >= p.B) return;
     const ns_stream_state st = p.state[b];
     bool active = !(st.flags & NS_ST_DONE);
-    if (!DECODE && active && st.bit_pos >= p.nbits[b]) {
+    if (!DECODE && !p.sample && active && st.bit_pos >= p.nbits[b]) {
         if (lane == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
         active = false;
     }
@@ -61,7 +61,8 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
     const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
     const int ntiles = (V + TS - 1) / TS;
     float r = 0.0f, m1 = -__builtin_inff(), m2 = -__builtin_inff();
-    double acc64 = 0.0;
+    double acc64 = 0.0, b64 = 0.0, u64 = 0.0;
+    const bool stats = p.stats != nullptr;
     int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
     for (int tile = 0; tile < ntiles; ++tile) {
         float x[W];
@@ -86,14 +87,22 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
             r = wave_max(mx);
             if (r == -__builtin_inff()) r = 0.0f;
         }
-        float a = 0.0f;
+        float a = 0.0f, bb = 0.0f, uu = 0.0f;
 #pragma unroll
         for (int q = 0; q < W; ++q) {
-            a += __builtin_amdgcn_exp2f((x[q] - r) * p.c32);
+            const float dx = fmaxf(x[q] - r, -3.0e38f);
+            const float e = __builtin_amdgcn_exp2f(dx * p.c32);
+            a += e;
+            if (stats) {
+                bb += e * dx;
+                uu += __builtin_amdgcn_exp2f(dx * L2E_F);
+            }
             m2 = fmaxf(m2, fminf(m1, x[q]));
             m1 = fmaxf(m1, x[q]);
         }
         acc64 += (double)a;
+        b64 += (double)bb;
+        u64 += (double)uu;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -102,6 +111,8 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
         m1 = fmaxf(m1, o1);
     }
     const double S_r = wave_sum_butterfly(acc64);
+    const double B_r = wave_sum_butterfly(b64);
+    const double U_r = wave_sum_butterfly(u64);
     double Sf = 0.0, S_lo = 0.0, S_hi = 0.0;
     const bool ok = fast_sum_interval(S_r, r, (double)(m1 + 0.0f), p.c32, p.inv_temp, W, Sf, S_lo, S_hi);
     if (lane == 0) {
@@ -115,6 +126,9 @@ __global__ __launch_bounds__(WPB* WAVE) void wide_stats_kernel(StepParams p, Wid
         w.S_fast = Sf;
         w.exact = (ok && !(p.flags & NS_STEP_FORCE_EXACT_SUM)) ? 0u : 1u;
         w.pad = 0;
+        w.S_r = S_r;
+        w.B_r = B_r;
+        w.U_r = U_r;
         ws[b] = w;
         count[b] = 0;
     }
@@ -134,7 +148,12 @@ __global__ __launch_bounds__(256) void wide_collect_kernel(StepParams p, const W
     const ns_stream_state st = p.state[b];
     const double thr = 1.0 / (double)(st.hi - st.lo);
     float xt;
-    if (w.exact) {
+    if (p.sample) {
+        // sampler support e_i >= 2^-60  <=>  x >= m + temp * ln(2^-60); widened (extra ids are harmless)
+        const double temp = 1.0 / p.inv_temp;
+        const double t = (double)w.m - temp * 41.58883083359672;
+        xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + temp * 41.58883083359672));
+    } else if (w.exact) {
         xt = -__builtin_inff();  // collect every valid id
     } else {
         // e(x) >= S_lo/R  <=>  x >= m + temp * ln(S_lo/R); widened generously (extra ids are harmless)
@@ -255,6 +274,42 @@ __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, dou
     return block_canonical_butterfly(sm64);
 }
 
+// block sum of one double per thread (statistics only: order not canonical)
+__device__ __forceinline__ double block_sum(double v, double* sm64) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if (lane == 0) sm64[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int i = 0; i < WIDE_THREADS / 64; ++i) r += sm64[i];
+    __syncthreads();
+    return r;
+}
+
+// statistics fallback (block version of wave_row_stats): float64 exps against the true max
+template <typename T>
+__device__ RowStats block_row_stats(const StepParams& p, const char* rowc, double m, double* sm64) {
+    double s1 = 0.0, st = 0.0, at = 0.0;
+    for (int j = threadIdx.x; j < p.V; j += WIDE_THREADS) {
+        if (is_banned(p, j)) continue;
+        const double d = (double)(Elem<T>::load1(rowc, j) + 0.0f) - m;
+        const double et = exp(d * p.inv_temp);
+        s1 += exp(d);
+        st += et;
+        at += et * (d * p.inv_temp);
+    }
+    s1 = block_sum(s1, sm64);
+    st = block_sum(st, sm64);
+    at = block_sum(at, sm64);
+    RowStats rs;
+    rs.lse1 = log(s1);
+    rs.lst = log(st);
+    rs.a_over_s = at / st;
+    return rs;
+}
+
 template <typename T, bool DECODE>
 __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, const WideStat* ws,
                                                                 const uint64_t* keys_sorted,
@@ -279,6 +334,81 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     const double Rd = (double)R;
     const double thr = 1.0 / Rd;
     auto e_of = [&](int i) -> double { return exp_canon(((double)wkey_val(sk[i]) - m) * p.inv_temp); };
+    RowStats rs{0.0, 0.0, 0.0};
+    const bool want_stats = !DECODE && p.stats != nullptr;
+    if (want_stats && !row_stats_from_stream(w.S_r, w.B_r, w.U_r, w.r, m, p.inv_temp, rs))
+        rs = block_row_stats<T>(p, rowc, m, sm64);
+
+    if (!DECODE && p.sample) {  // sampler (oracle steps S2-S5): support, canonical E, 2^48 CDF, one draw
+        int fl = Kc;
+        for (int i = tid; i < Kc; i += WIDE_THREADS)
+            if (e_of(i) < SAMPLE_SUPPORT && i < fl) fl = i;
+        const int ks = block_min_int(fl, smi);
+        double acc = 0.0;
+        for (int base = 0; base < ks; base += WIDE_ROUND) {
+            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < ks) ? e_of(base + i) : 0.0;
+            __syncthreads();
+            if (tid < 64)
+                for (int i = tid; i < WIDE_ROUND && base + i < ks; i += 64) acc += ebuf[i];
+            __syncthreads();
+        }
+        if (tid < 64) sm64[tid] = acc;
+        __syncthreads();
+        const double E = block_canonical_butterfly(sm64);
+        const int cs = (ks + WIDE_THREADS - 1) / WIDE_THREADS;
+        const int i0 = min(ks, tid * cs), i1 = min(ks, i0 + cs);
+        auto q_of = [&](int i) -> int64_t { return (int64_t)__builtin_rint((e_of(i) / E) * SAMPLE_SCALE); };
+        int64_t local = 0;
+        for (int i = i0; i < i1; ++i) local += q_of(i);
+        int64_t total;
+        const int64_t pre = block_excl_scan(local, sml, total);
+        const uint64_t u = rand64(p.seed, p.stream_offset + b, st.ntokens);
+        const uint64_t idx = __umul64hi(u, (uint64_t)total);
+        int sel_l = 0x7FFFFFFF;
+        {
+            int64_t c = pre;
+            for (int i = i0; i < i1; ++i) {
+                c += q_of(i);
+                if ((uint64_t)c > idx) {
+                    sel_l = i;
+                    break;
+                }
+            }
+        }
+        const int sel = block_min_int(sel_l, smi);
+        double kl = 0.0, h = 0.0;
+        if (want_stats) {
+            const double logE = log(E);
+            for (int i = i0; i < i1; ++i) {
+                const double xi = (double)wkey_val(sk[i]) - m;
+                const double lq = xi * p.inv_temp - logE;
+                const double q = e_of(i) / E;
+                kl += q * (lq - (xi - rs.lse1));
+                h += q * lq;
+            }
+            kl = block_sum(kl, sm64);
+            h = block_sum(h, sm64);
+        }
+        if (tid != 0) return;
+        const int32_t token = (int32_t)wkey_id(sk[sel]);
+        ns_stream_state ns = st;
+        ns.ntokens = st.ntokens + 1;
+        p.state[b] = ns;
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        if (p.trace) {
+            ns_step_trace tr = {Kc, ks, sel, 0, token, 0, E};
+            p.trace[b] = tr;
+        }
+        if (want_stats) {
+            double* a = p.stats + 4 * (int64_t)b;
+            a[0] += ((double)wkey_val(sk[sel]) - m) - rs.lse1;
+            a[1] += kl / 0.69315;
+            a[2] += -h / 0.69315;
+            a[3] += 1.0;
+        }
+        return;
+    }
 
     // ---- 1. cutoff k0 = first rank with e_i/S < thr (ranks >= Kc are below for certain)
     bool exact = w.exact != 0;
@@ -389,6 +519,18 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     }
     const int sel = block_min_int(sel_l, smi);
     if (sel == 0x7FFFFFFF) err = DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE;
+    // statistics of an encode step (arithmetic.py:193-199): KL(q || p) over the k' kept entries
+    double kl = 0.0;
+    if (want_stats && !err) {
+        const int64_t deficit = (int64_t)R - cum_at[0];
+        for (int i = i0; i < min(i1, kp); ++i) {
+            int64_t pf = q_of(i);
+            if (i == 0) pf += deficit;
+            const double qd = (double)pf / Rd;
+            if (qd > 0.0) kl += qd * (log(qd) - (((double)wkey_val(sk[i]) - m) - rs.lse1));
+        }
+    }
+    if (want_stats) kl = block_sum(kl, sm64);
     if (!err) {
         if (sel - 1 >= i0 && sel - 1 < i1) cum_at[1] = cum_upto(sel - 1);
         if (sel >= i0 && sel < i1) cum_at[2] = cum_upto(sel);
@@ -441,6 +583,13 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     if (p.trace) {
         ns_step_trace tr = {k, kp, sel, n, token, exact ? 1 : 0, S_used};
         p.trace[b] = tr;
+    }
+    if (want_stats) {
+        double* a = p.stats + 4 * (int64_t)b;
+        a[0] += ((double)wkey_val(sel_key) - m) - rs.lse1;
+        a[1] += kl / 0.69315;
+        a[2] += (rs.lst - rs.a_over_s) / 0.69315;
+        a[3] += 1.0;
     }
     if (p.counters && exact) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1))], 1ull);
 }
