@@ -124,6 +124,13 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
  * is_sent_finish).  The caller keeps it alive; NULL clears it. */
 int ns_set_sentence_end(ns_ctx* ctx, const uint8_t* d_table);
 
+/* Rank export for decode repair: when a later ns_decode_step finds stream b's received token outside the
+ * kept top-k' (NS_ST_ERR_DIVERGE; the state is left unchanged so the step can be re-issued), the kernel
+ * writes the kept ids in rank order to d_ranked[b*stride + i], i < k', followed by -1 (truncated at
+ * stride).  The host runs the reference's BPE-repair heuristics on them (code_base/arithmetic.py:300-342)
+ * and re-issues the step with the repaired token.  d_ranked is a DEVICE int32 array; NULL switches it off. */
+int ns_set_rank_export(ns_ctx* ctx, int32_t* d_ranked, int stride);
+
 /* Statistics of the encode steps (code_base/arithmetic.py:193-199, returned by encode_arithmetic :217):
  * d_stats is a DEVICE array [B][4] of doubles that every later ns_encode_step accumulates into, per
  * stream: [0] sum of log p(selected) under the untempered softmax, [1] sum of KL(q || p) in bits over the

@@ -26,7 +26,7 @@ NS_STEP_DIAG_STREAM_ONLY, NS_STEP_DIAG_NO_CANDIDATES, NS_STEP_DIAG_SKIP_CDF = 2,
 NS_MAX_BANNED = 8
 
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
-           "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step",
+           "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_read_counters")
 
 
@@ -83,6 +83,8 @@ def lib() -> ctypes.CDLL:
                                  ctypes.c_double, ctypes.c_int, i32p, ctypes.c_int, vp, ctypes.c_uint32, vp]
     L.ns_set_sentence_end.restype = ctypes.c_int
     L.ns_set_sentence_end.argtypes = [vp, vp]
+    L.ns_set_rank_export.restype = ctypes.c_int
+    L.ns_set_rank_export.argtypes = [vp, vp, ctypes.c_int]
     L.ns_set_stats.restype = ctypes.c_int
     L.ns_set_stats.argtypes = [vp, vp]
     L.ns_sample_step.restype = ctypes.c_int

@@ -253,6 +253,13 @@ class EncodeSession:
     def all_done(self) -> bool:
         return bool(np.all(_state_fields(self.state)["flags"] & _lib.NS_ST_DONE))
 
+    def mark_done(self, streams: Sequence[int]) -> None:
+        """Stop ``streams`` (host decision, e.g. the reference's '<eos>' text check, arithmetic.py:208-210)."""
+        torch = _torch()
+        idx = torch.tensor(list(streams), device=self.state.device, dtype=torch.long)
+        w = self.state.view(torch.int32)
+        w[idx, 7] = w[idx, 7] | _lib.NS_ST_DONE
+
     def ensure_history(self, steps_ahead: int) -> None:
         """Grow the device token history so ``steps_ahead`` more steps fit (finish_sent tails are unbounded)."""
         need = int(self.fields()["ntokens"].max(initial=0)) + int(steps_ahead)
@@ -453,3 +460,75 @@ def sample_batch(ctx: CoderContext, B: int, length: int, logits_fn, *, seed: int
     for t in range(length):
         last = sess.step(logits_fn(t, last))
     return sess.tokens(), (sess.stats() if stats else None)
+
+
+class StreamingDecodeSession:
+    """Decode with the received tokens supplied step by step by the host (``code_base/arithmetic.py:254-371``
+    loop, where the token list can change mid-stream: the BPE repair of ``:300-342`` inserts and deletes
+    tokens).  A stream whose token falls outside the kept top-k' is flagged NS_ST_ERR_DIVERGE with its state
+    untouched and its ranked kept ids exported; :meth:`clear` re-arms it for a re-issued step."""
+
+    def __init__(self, ctx: CoderContext, B: int, max_tokens: int):
+        torch = _torch()
+        if B < 1 or B > ctx.max_batch:
+            raise ConfigurationError(f"batch {B} outside [1, {ctx.max_batch}]")
+        self.ctx, self.B = ctx, int(B)
+        dev = torch.device("cuda", ctx.device)
+        self.dev = dev
+        P = ctx.params.precision
+        self.out_stride = int((max(1, max_tokens) * P + P + 7) // 8 + 8)
+        self.out_bits = torch.zeros((self.B, self.out_stride), dtype=torch.uint8, device=dev)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        self.rank_stride = int(ctx.K) + 1
+        self.ranked = torch.full((self.B, self.rank_stride), -1, dtype=torch.int32, device=dev)
+
+    def _grow(self, need_bits: int) -> None:
+        torch = _torch()
+        need = (need_bits + 7) // 8 + 8
+        if need <= self.out_stride:
+            return
+        new = torch.zeros((self.B, max(need, 2 * self.out_stride)), dtype=torch.uint8, device=self.dev)
+        new[:, : self.out_stride] = self.out_bits
+        self.out_bits, self.out_stride = new, new.shape[1]
+
+    def step(self, logits, tokens: Sequence[int], is_last: Sequence[bool], active: Sequence[bool]) -> None:
+        torch = _torch()
+        p = self.ctx.params
+        f = _state_fields(self.state)
+        self._grow(int(f["bit_pos"].max(initial=0)) + 2 * p.precision)
+        tok = torch.tensor(np.asarray(tokens, dtype=np.int32), device=self.dev)
+        last = torch.tensor(np.asarray(is_last, dtype=np.uint8), device=self.dev)
+        act = torch.tensor(np.asarray(active, dtype=np.uint8), device=self.dev)
+        L = _lib.lib()
+        self.ctx.check(L.ns_set_rank_export(self.ctx._h, _ptr(self.ranked), self.rank_stride), "ns_set_rank_export")
+        rc = L.ns_decode_step(self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(tok), _ptr(last), _ptr(act),
+                              _ptr(self.state), _ptr(self.out_bits), self.out_stride, float(p.temp), int(p.topk),
+                              self.ctx._banned, self.ctx._nbanned, ctypes.c_void_p(0), 0, _stream_handle())
+        L.ns_set_rank_export(self.ctx._h, ctypes.c_void_p(0), 0)
+        self.ctx.check(rc, "ns_decode_step")
+
+    def diverged(self) -> List[int]:
+        f = _state_fields(self.state)["flags"]
+        return np.nonzero(f & _lib.NS_ST_ERR_DIVERGE)[0].tolist()
+
+    def ranked_ids(self, b: int) -> List[int]:
+        row = self.ranked[b].cpu().numpy()
+        end = np.nonzero(row < 0)[0]
+        return row[: int(end[0]) if end.size else row.size].astype(np.int64).tolist()
+
+    def clear(self, streams: Sequence[int]) -> None:
+        """Drop the divergence / done flags of ``streams`` (their lo/hi/bit_pos were left untouched)."""
+        if not streams:
+            return
+        torch = _torch()
+        w = self.state.view(torch.int32)
+        idx = torch.tensor(list(streams), device=self.dev, dtype=torch.long)
+        keep = ~(_lib.NS_ST_ERR_DIVERGE | _lib.NS_ST_DONE)
+        w[idx, 7] = w[idx, 7] & keep
+
+    def bits(self) -> List[List[int]]:
+        f = _state_fields(self.state)
+        ob = self.out_bits.cpu().numpy()
+        return [np.unpackbits(ob[i], bitorder="little")[: int(f["bit_pos"][i])].astype(np.int64).tolist()
+                for i in range(self.B)]

@@ -891,7 +891,18 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
                 }
             }
         }
-        if (sel < 0) err = NS_ST_ERR_DIVERGE;
+        if (sel < 0) {
+            err = NS_ST_ERR_DIVERGE;
+            if (p.ranked) {  // export the ranked kept ids for the host's BPE repair (arithmetic.py:300-342)
+                int32_t* rk_out = p.ranked + (int64_t)b * p.ranked_stride;
+#pragma unroll
+                for (int s = 0; s < NSK; ++s) {
+                    const int i = s * WAVE + lane;
+                    if (s < nsk && i < kp && i < p.ranked_stride) rk_out[i] = (int32_t)key_id(sk[s]);
+                }
+                if (lane == 0 && kp < p.ranked_stride) rk_out[kp] = -1;
+            }
+        }
     }
 
     uint64_t tk = 0;
@@ -1153,6 +1164,8 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->wide = NsgWide();
     ctx->sent_end = nullptr;
     ctx->stats = nullptr;
+    ctx->ranked = nullptr;
+    ctx->ranked_stride = 0;
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
@@ -1299,6 +1312,8 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
     p.in_token = d_in_token;
     p.is_last = d_is_last;
     p.active = d_active;
+    p.ranked = ctx->ranked;
+    p.ranked_stride = ctx->ranked_stride;
     p.out_bits = d_out_bits;
     p.out_stride = out_stride;
     const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, true, (hipStream_t)hip_stream)
@@ -1327,6 +1342,13 @@ int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_
     const bool ok = p.K > ns_max_topk(ctx->dtype) ? nsg_wide_launch(ctx, p, false, (hipStream_t)hip_stream)
                                                   : launch<false>(ctx, p, (hipStream_t)hip_stream);
     if (!ok) return fail(ctx, NS_ERR_HIP, "ns_sample_step: launch failed");
+    return NS_OK;
+}
+
+int ns_set_rank_export(ns_ctx* ctx, int32_t* d_ranked, int stride) {
+    if (!ctx || (d_ranked && stride < 2)) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_export: bad argument");
+    ctx->ranked = d_ranked;
+    ctx->ranked_stride = d_ranked ? stride : 0;
     return NS_OK;
 }
 

@@ -179,6 +179,9 @@ struct StepParams {
     int64_t stream_offset;
     // statistics sink [B][4]: sum log p(sel), sum KL bits, sum entropy bits, steps (nullable)
     double* stats;
+    // decode: ranked ids of a diverged stream (ranks < k', then -1), [B][ranked_stride] (nullable)
+    int32_t* ranked;
+    int ranked_stride;
     // common
     ns_stream_state* state;
     ns_step_trace* trace;

@@ -49,6 +49,8 @@ struct ns_ctx {
     NsgWide wide;
     const uint8_t* sent_end;  // device table [vocab] for NS_STEP_FINISH_SENT (ns_set_sentence_end)
     double* stats;            // encode statistics sink [B][4] (ns_set_stats), nullable
+    int32_t* ranked;          // decode rank export [B][ranked_stride] (ns_set_rank_export), nullable
+    int ranked_stride;
     std::string err;
 };
 

@@ -519,6 +519,11 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     }
     const int sel = block_min_int(sel_l, smi);
     if (sel == 0x7FFFFFFF) err = DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE;
+    if (DECODE && err && p.ranked) {  // ranked kept ids for the host's BPE repair (arithmetic.py:300-342)
+        int32_t* rk_out = p.ranked + (int64_t)b * p.ranked_stride;
+        for (int i = tid; i < kp && i < p.ranked_stride; i += WIDE_THREADS) rk_out[i] = (int32_t)wkey_id(sk[i]);
+        if (tid == 0 && kp < p.ranked_stride) rk_out[kp] = -1;
+    }
     // statistics of an encode step (arithmetic.py:193-199): KL(q || p) over the k' kept entries
     double kl = 0.0;
     if (want_stats && !err) {

@@ -17,7 +17,7 @@ from __future__ import annotations
 from collections import deque
 from typing import Deque, Dict, Iterable, List, Mapping, Optional, Sequence
 
-from ..coder import CoderContext, CoderParams, DecodeSession, EncodeSession
+from ..coder import CoderContext, CoderParams, DecodeSession, EncodeSession, SampleSession, StreamingDecodeSession
 from ..exceptions import ConfigurationError
 
 CodecState = Dict[str, object]
@@ -83,7 +83,27 @@ class HipArithmeticLM:
             raise NativeLibraryError("HipArithmeticLM needs a ROCm GPU (the coder has no CPU path)")
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         ldt = torch.float16 if logits_dtype == "f16" else torch.float32
-        self.lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
+        lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
+        self._init(lm, tokenizer, dev, logits_dtype, banned, max_batch)
+
+    @classmethod
+    def from_batched(cls, batched_lm, tokenizer=None, *, logits_dtype: str = "f32",
+                     banned: Optional[Sequence[int]] = None, max_batch: int = 4096) -> "HipArithmeticLM":
+        """Provider over any batched-logits LM with the ``prefill(context, B, max_new)`` / ``step(tokens)``
+        protocol (e.g. :class:`~neuralsteganography_amd.synthetic.SyntheticBatchedLM`)."""
+        import torch
+
+        if not torch.cuda.is_available():
+            from .._lib import NativeLibraryError
+
+            raise NativeLibraryError("HipArithmeticLM needs a ROCm GPU (the coder has no CPU path)")
+        self = cls.__new__(cls)
+        self._init(batched_lm, tokenizer, torch.device("cuda", torch.cuda.current_device()), logits_dtype, banned,
+                   max_batch)
+        return self
+
+    def _init(self, lm, tokenizer, dev, logits_dtype, banned, max_batch) -> None:
+        self.lm = lm
         self.vocab = self.lm.shape.vocab
         self.tokenizer = tokenizer if tokenizer is not None else ByteTokenizer(self.vocab)
         self.logits_dtype = logits_dtype
@@ -161,7 +181,7 @@ class HipArithmeticLM:
     # ---------------------------------------------------------------- batched entry points
     def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], check_every: int = 16,
-                     stall_steps: int = 4096) -> List[List[int]]:
+                     stall_steps: int = 4096, return_stats: bool = False, stop_text: Optional[str] = None):
         """Encode B independent bit lists in lockstep (one GPT-2 forward + one coder launch per token).
 
         The reference coder has no underflow handling: when the interval straddles the midpoint and one
@@ -180,11 +200,25 @@ class HipArithmeticLM:
         budget = 2 * max_bits + 64            # initial KV/history capacity (grows on demand)
         hard_cap = 64 * max_bits + 4096       # a stream fixing < 1/64 bit per token is reported, not looped
         logits = self.lm.prefill(context, B, budget)
-        sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap)
+        sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap, stats=return_stats)
         t = 0
         last_pos = None
         last_move = 0
+        outs: List[List[int]] = [[] for _ in range(B)]
         while True:
+            if stop_text is not None and t > 0:
+                # code_base/arithmetic.py:207-210: a stream stops once its decoded cover text contains
+                # stop_text ('<eos>' in the message->bits mode of run_single.py).  Checked on a decoded tail.
+                f = sess.fields()
+                tok = sess.out_token.cpu().numpy()
+                stop = []
+                for i in range(B):
+                    if not (f["flags"][i] & 1) and len(outs[i]) < int(f["ntokens"][i]):
+                        outs[i].append(int(tok[i]))
+                        if stop_text in self.tokenizer.decode(outs[i][-16:]):
+                            stop.append(i)
+                if stop:
+                    sess.mark_done(stop)
             if t % check_every == 0:
                 f = sess.fields()
                 if bool((f["flags"] & 1).all()):
@@ -212,6 +246,8 @@ class HipArithmeticLM:
             st = _bits_count_state(len(b))
             self._encode_states.append(st)
             self._decode_states.append(dict(st))
+        if return_stats:
+            return toks, sess.stats()
         return toks
 
     def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
@@ -238,4 +274,115 @@ class HipArithmeticLM:
         return sess.bits()
 
 
-__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality"]
+    def decode_tokens_repair(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                             quality: Mapping[str, object], enc=None) -> List[List[int]]:
+        """Batched ``decode_arithmetic`` token loop with the reference's BPE repair (code_base/arithmetic.py
+        :254-371): a received token outside the kept top-k' is repaired on the host from the kernel's
+        ranked ids (:300-342, :func:`bpe_repair`), the token list is edited as the reference edits it, and
+        the step is re-issued; an unrepairable token decodes as rank 0 while the LM is still fed the
+        received token, exactly as the reference does.  Returns every emitted bit per stream."""
+        import torch
+
+        enc = enc if enc is not None else self.tokenizer
+        lists = [[int(t) for t in tl] for tl in token_lists]
+        B = len(lists)
+        if B == 0:
+            return []
+        params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
+        ctx = self._coder(params, B)
+        sess = StreamingDecodeSession(ctx, B, max_tokens=max(len(x) for x in lists) + 8)
+        logits = self.lm.prefill(context, B, max(len(x) for x in lists) + 8)
+        pos = [0] * B
+        while True:
+            active = [pos[b] < len(lists[b]) for b in range(B)]
+            if not any(active):
+                break
+            for b in range(B):
+                if active[b] and not 0 <= lists[b][pos[b]] < self.vocab:
+                    raise ConfigurationError(f"received token id outside [0, {self.vocab})")
+            tok = [lists[b][pos[b]] if active[b] else 0 for b in range(B)]
+            last = [active[b] and pos[b] == len(lists[b]) - 1 for b in range(B)]
+            sess.step(logits, tok, last, active)
+            feed = list(tok)
+            bad = sess.diverged()
+            if bad:
+                redo = [0] * B
+                for b in bad:
+                    ids = sess.ranked_ids(b)
+                    coder_tok, fixed = bpe_repair(enc, lists[b], pos[b], ids)
+                    redo[b] = coder_tok
+                    feed[b] = lists[b][pos[b]]  # repaired token, or the received one when unrepairable
+                sess.clear(bad)
+                act2 = [b in bad for b in range(B)]
+                last2 = [act2[b] and pos[b] == len(lists[b]) - 1 for b in range(B)]
+                sess.step(logits, redo, last2, act2)
+                still = sess.diverged()
+                if still:
+                    from ..codec.errors import DecodeDivergenceError
+
+                    raise DecodeDivergenceError(f"streams {still[:8]}: repaired token still outside the top-k")
+            for b in range(B):
+                if active[b]:
+                    pos[b] += 1
+            if any(pos[b] < len(lists[b]) for b in range(B)):
+                logits = self.lm.step(torch.tensor(feed, device=self.device, dtype=torch.long))
+        return sess.bits()
+
+    def sample_batch(self, B: int, length: int, context: Sequence[int], *, temperature: float = 1.0,
+                     topk: int = -1, seed: int = 0, stream_offset: int = 0, stats: bool = True):
+        """B independent non-stego samples of ``length`` tokens from one context (code_base/sample.py, batched):
+        returns ``(token lists, per-stream {avg_NLL, avg_KL, avg_Hq})``."""
+        import torch
+
+        params = CoderParams(vocab=self.vocab, precision=16, temp=float(temperature),
+                             topk=int(topk) if int(topk) > 0 else self.vocab, dtype=self.logits_dtype,
+                             banned=self.banned)
+        ctx = self._coder(params, B)
+        sess = SampleSession(ctx, B, seed=seed, topk=topk, temp=temperature, stream_offset=stream_offset,
+                             max_tokens=max(1, length), stats=stats)
+        logits = self.lm.prefill(context, B, length + 1)
+        for t in range(length):
+            tok = sess.step(logits)
+            if t + 1 < length:
+                logits = self.lm.step(tok.to(torch.long))
+        return sess.tokens(), (sess.stats() if stats else None)
+
+
+def bpe_repair(enc, inp: List[int], i: int, ranked_ids: Sequence[int]):
+    """The reference's BPE repair for a received token outside the kept top-k (code_base/arithmetic.py:300-342),
+    restated line for line over ``ranked_ids`` (the kernel's ranked kept ids).  Edits ``inp`` in place as the
+    reference does -- including its deletion loop, which removes every other following token when more than
+    one is merged -- and returns ``(token to decode, repaired?)``; unrepairable tokens decode as rank 0."""
+    true_token_text = enc.decode([inp[i]])
+    for cand in ranked_ids:
+        cand = int(cand)
+        prop_token_text = enc.decode([cand])
+        if inp[i] == 128 and cand == 198:  # common case that is not caught
+            inp[i] = cand
+            return cand, True
+        if len(prop_token_text) <= len(true_token_text) and \
+                prop_token_text == true_token_text[:len(prop_token_text)]:
+            suffix = true_token_text[len(prop_token_text):]
+            suffix_tokens = enc.encode(suffix)
+            inp[i] = cand
+            inp[i + 1:i + 1] = suffix_tokens
+            return cand, True
+        elif len(prop_token_text) > len(true_token_text) and \
+                true_token_text == prop_token_text[:len(true_token_text)]:
+            whole_text = true_token_text
+            num_extra = 1
+            while len(whole_text) < len(prop_token_text):
+                whole_text += enc.decode([inp[i + num_extra]])
+                num_extra += 1
+            if prop_token_text == whole_text[:len(prop_token_text)]:
+                inp[i] = cand
+                for j in range(1, num_extra):
+                    del inp[i + j]
+                if len(whole_text) > len(prop_token_text):
+                    suffix = whole_text[len(prop_token_text):]
+                    inp[i + 1:i + 1] = enc.encode(suffix)
+                return cand, True
+    return int(ranked_ids[0]), False
+
+
+__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality", "bpe_repair"]

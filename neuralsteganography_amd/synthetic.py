@@ -80,3 +80,39 @@ def top_region_tie_free(row: np.ndarray, topk: int, banned: Sequence[int]) -> bo
     n = min(topk + 1, vals.size)
     top = np.sort(vals)[::-1][:n]
     return bool(np.all(top[:-1] != top[1:]))
+
+
+class SyntheticBatchedLM:
+    """Batched-logits provider with context-independent synthetic rows (the ``prefill``/``step`` protocol of
+    :class:`~neuralsteganography_amd.lm.gpt2.BatchedGPT2`): call t (prefill = call 0) returns
+    ``logits_row(seed, streams[b], t)`` for every stream b, whatever tokens were fed -- the same rows the
+    golden generator's synthetic model hands the reference coder (tests/golden/make_golden.py)."""
+
+    def __init__(self, seed: int, vocab: int, scale: float = 3.0, dtype: str = "f32", streams=None, boost=None):
+        from types import SimpleNamespace
+
+        self.boost = {int(k): int(v) for k, v in (boost or {}).items()}  # call index -> token id, +30 logit
+        self.seed, self.vocab, self.scale = int(seed), int(vocab), float(scale)
+        self.np_dtype = np.float16 if dtype == "f16" else np.float32
+        self.ld = ((self.vocab + 63) // 64) * 64
+        self.shape = SimpleNamespace(vocab=self.vocab, n_positions=1024)
+        self.streams = None if streams is None else [int(s) for s in streams]
+        self.t, self.B, self.fed = 0, 0, []
+
+    def _rows(self):
+        import torch
+
+        ids = self.streams[: self.B] if self.streams is not None else list(range(self.B))
+        arr = logits_batch(self.seed, ids, self.t, self.vocab, self.scale, self.np_dtype, self.ld)
+        if self.t in self.boost:
+            arr[:, self.boost[self.t]] += self.np_dtype(30.0)
+        return torch.from_numpy(arr).cuda()
+
+    def prefill(self, context, B: int, max_new: int):
+        self.t, self.B, self.fed = 0, int(B), []
+        return self._rows()
+
+    def step(self, tokens):
+        self.fed.append(tokens.detach().cpu().numpy().copy())
+        self.t += 1
+        return self._rows()

@@ -63,16 +63,20 @@ def _import_reference():
 class SyntheticModel:
     """Synthetic LM: call ``t`` returns row ``logits_row(seed, stream, t)`` (context is ignored)."""
 
-    def __init__(self, seed, stream, vocab, scale, dtype):
+    def __init__(self, seed, stream, vocab, scale, dtype, boost=None):
         import torch
 
         self.torch = torch
         self.seed, self.stream, self.vocab, self.scale, self.dtype = seed, stream, vocab, scale, dtype
+        self.boost = dict(boost or {})  # call index -> token id whose logit gets +30
         self.calls = 0
         self.config = types.SimpleNamespace(n_positions=1024)
 
     def __call__(self, input_ids, past_key_values=None, use_cache=True, position_ids=None):
         row = synthetic.logits_row(self.seed, self.stream, self.calls, self.vocab, self.scale, self.dtype)
+        if self.calls in self.boost:
+            row = row.copy()
+            row[self.boost[self.calls]] += 30.0
         self.calls += 1
         T = int(input_ids.shape[-1])
         logits = self.torch.zeros((1, T, self.vocab), dtype=self.torch.from_numpy(row).dtype)
@@ -136,6 +140,16 @@ SAMPLE_CONFIGS = {
     "s4_v700_f32_k690_t07": dict(vocab=700, dtype="f32", scale=2.0, temp=0.7, topk=690, lengths=[64]),
 }
 SAMPLE_TORCH_SEED = 1234
+
+# code_base compat (neuralsteganography_amd/code_base.py): encode -> cover text -> decode through the toy
+# tokenizer (tests/golden/toy_tokenizer.py), whose re-tokenisation triggers the decode repair
+# (arithmetic.py:300-342); "eos" boosts token 650 ("<eos>") at one step so the '<eos>' stop (:207-210) fires.
+COMPAT_CONFIGS = {
+    "c1_toy_v700_repair": dict(vocab=700, dtype="f32", scale=2.0, temp=1.0, precision=16, topk=600,
+                               nbits=[64, 40, 24, 96]),
+    "c2_toy_v700_eos": dict(vocab=700, dtype="f32", scale=2.0, temp=1.0, precision=16, topk=600,
+                            nbits=[200], boost={5: 650}),
+}
 
 
 class SampleModel(SyntheticModel):
@@ -204,8 +218,58 @@ def run_sample_config(name, cfg, stable_sort_mode):
     return out
 
 
+def run_compat_config(name, cfg, ref, stable_sort_mode):
+    from tests.golden.toy_tokenizer import ToyTokenizer
+
+    enc = ToyTokenizer(cfg["vocab"])
+    V = cfg["vocab"]
+    context = synthetic.DEFAULT_CONTEXT
+    out = {"tokens": [], "tok_off": [0], "bits": [], "bit_off": [0], "msg": [], "msg_off": [0], "stats": [],
+           "text": [], "text_off": [0]}
+    for s, nbits in enumerate(cfg["nbits"]):
+        msg = synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, (nbits + 7) // 8))[:nbits]
+        boost = {int(k): v for k, v in cfg.get("boost", {}).items()}
+        model = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], np.float32, boost=boost)
+        with stable_sort_mode():
+            toks, nll, kl_, wpb, hq = ref.encode_arithmetic(model, enc, list(msg), context, device="cpu",
+                                                            temp=cfg["temp"], precision=cfg["precision"],
+                                                            topk=cfg["topk"])
+        text = enc.decode(toks)
+        dmodel = SyntheticModel(LOGIT_SEED, s, V, cfg["scale"], np.float32, boost=boost)
+        with stable_sort_mode():
+            bits = ref.decode_arithmetic(dmodel, enc, text, context, device="cpu", temp=cfg["temp"],
+                                         precision=cfg["precision"], topk=cfg["topk"])
+        retok = enc.encode(text)
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["bits"] += list(bits); out["bit_off"].append(len(out["bits"]))
+        out["msg"] += list(msg); out["msg_off"].append(len(out["msg"]))
+        out["stats"].append([nll, kl_, wpb, hq])
+        tb = list(text.encode("utf-8"))
+        out["text"] += tb; out["text_off"].append(len(out["text"]))
+        print(f"  {name} s={s} nbits={nbits} tokens={len(toks)} retokenised={len(retok)} "
+              f"same={retok == list(toks)} decoded={len(bits)} roundtrip={bits[:nbits] == list(msg)}", flush=True)
+    return out
+
+
 def main(names=None):
     ref, stable = _import_reference()
+    for name, cfg in COMPAT_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_compat_config(name, cfg, ref, stable)
+        meta = dict(cfg, name=name, kind="compat", logit_seed=LOGIT_SEED, payload_seed=synthetic.PAYLOAD_SEED,
+                    context=synthetic.DEFAULT_CONTEXT, banned=[cfg["vocab"] - 1, 628], tokenizer="ToyTokenizer",
+                    reference="code_base/arithmetic.py encode_arithmetic -> text -> decode_arithmetic",
+                    sort="stable (value desc, id asc)")
+        meta["boost"] = {str(k): v for k, v in cfg.get("boost", {}).items()}
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            bits=np.asarray(res["bits"], dtype=np.uint8), bit_off=np.asarray(res["bit_off"], np.int64),
+            msg=np.asarray(res["msg"], dtype=np.uint8), msg_off=np.asarray(res["msg_off"], np.int64),
+            stats=np.asarray(res["stats"], dtype=np.float64),
+            text=np.asarray(res["text"], dtype=np.uint8), text_off=np.asarray(res["text_off"], np.int64))
     for name, cfg in SAMPLE_CONFIGS.items():
         if names and name not in names:
             continue
