@@ -11,4 +11,30 @@ class ConfigurationError(NeuralStegoError):
     """Invalid user configuration (``exceptions.py:12``)."""
 
 
-__all__ = ["NeuralStegoError", "ConfigurationError"]
+class FramingError(NeuralStegoError):
+    """Packet framing or chunk assembly failed (``exceptions.py:16``)."""
+
+
+class PacketECCError(FramingError):
+    """Reed-Solomon decoding (or the packet envelope) failed irrecoverably (``exceptions.py:20``)."""
+
+
+class PacketCRCError(FramingError):
+    """CRC32 verification failed (``exceptions.py:24``)."""
+
+
+class MissingChunksError(FramingError):
+    """Some packets of a message never arrived (``exceptions.py:28-35``); ``partial_payload`` holds the
+    payloads that did, in sequence order."""
+
+    def __init__(self, missing_indices, partial_payload: bytes = b""):
+        self.missing_indices = list(missing_indices)
+        self.partial_payload = bytes(partial_payload)
+        super().__init__(self.missing_indices, self.partial_payload)
+
+    def __str__(self) -> str:
+        return "Missing chunks at indices: " + ", ".join(str(i) for i in self.missing_indices)
+
+
+__all__ = ["NeuralStegoError", "ConfigurationError", "FramingError", "PacketECCError", "PacketCRCError",
+           "MissingChunksError"]

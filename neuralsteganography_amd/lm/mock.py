@@ -1,40 +1,31 @@
-"""Deterministic mock provider (config C1), mirroring ``src/neuralstego/lm/mock.py:36-59``.
+"""C1 provider: the identity coder behind ``load_lm("mock")`` (behaviour of ``src/neuralstego/lm/mock.py``).
 
-Identity coder: packet bytes are the token ids.  It runs no GPU code and exists so that the drop-in
-registry answers ``load_lm("mock")`` exactly like the reference.
+Cover tokens ARE the packet bytes: ``encode_arithmetic`` packs the LSB-first bit list into bytes and returns
+their values; ``decode_arithmetic`` unpacks token values (mod 256) back into bits.  Pure host code (no model,
+no GPU); it exists so framing and api tests run anywhere, as in the reference.
 """
 
 from __future__ import annotations
 
 from typing import Dict, Iterable, List
 
+import numpy as np
+
 
 class MockTokenizer:
+    """UTF-8 bytes as token ids."""
+
     def encode(self, text: str) -> List[int]:
-        return list(text.encode("utf-8"))
+        return [int(v) for v in text.encode("utf-8")]
 
     def decode(self, tokens: Iterable[int]) -> str:
-        return bytes(int(t) % 256 for t in tokens).decode("utf-8", errors="ignore")
-
-
-def _bits_to_bytes(bits: Iterable[int]) -> bytes:
-    data = list(bits)
-    if len(data) % 8:
-        raise ValueError("bit stream length must be a multiple of 8")
-    out = bytearray()
-    for i in range(0, len(data), 8):
-        v = 0
-        for off, bit in enumerate(data[i : i + 8]):
-            v |= (int(bit) & 1) << off
-        out.append(v)
-    return bytes(out)
-
-
-def _bytes_to_bits(data: bytes) -> List[int]:
-    return [(byte >> i) & 1 for byte in data for i in range(8)]
+        raw = np.asarray(list(tokens), dtype=np.int64) % 256
+        return raw.astype(np.uint8).tobytes().decode("utf-8", errors="ignore")
 
 
 class MockLM:
+    """Identity packet-bytes <-> tokens provider (api ``LMProvider`` protocol)."""
+
     def __init__(self) -> None:
         self.tokenizer = MockTokenizer()
 
@@ -42,12 +33,18 @@ class MockLM:
         return self.tokenizer.encode(text)
 
     def encode_arithmetic(self, bits: List[int], context: List[int], *, quality: Dict[str, float]) -> List[int]:
-        _ = context, quality
-        return [int(b) for b in _bits_to_bytes(bits)] if bits else []
+        del context, quality
+        if len(bits) % 8:
+            raise ValueError("bit stream length must be a multiple of 8")
+        if not bits:
+            return []
+        packed = np.packbits(np.asarray(bits, dtype=np.uint8) & 1, bitorder="little")
+        return packed.astype(np.int64).tolist()
 
     def decode_arithmetic(self, tokens: List[int], context: List[int], *, quality: Dict[str, float]) -> List[int]:
-        _ = context, quality
-        return _bytes_to_bits(bytes(int(t) % 256 for t in tokens))
+        del context, quality
+        raw = (np.asarray(list(tokens), dtype=np.int64) % 256).astype(np.uint8)
+        return np.unpackbits(raw, bitorder="little").astype(np.int64).tolist()
 
 
 __all__ = ["MockLM", "MockTokenizer"]

@@ -165,3 +165,17 @@ def test_provider_finish_sent_without_sentence_end_is_reported():
     with pytest.raises(ArithmeticRangeError, match="finish_sent"):
         lm.encode_batch(bits, lm.encode_seed(""), quality={"temp": 1.0, "precision": 20, "topk": 100,
                                                             "finish_sent": True}, stall_steps=64)
+
+
+def test_batched_front_end_multi_message_roundtrip():
+    """stego_encode_batch / stego_decode_batch (api.py:707-807 batched): every packet of every message is a
+    stream of one lockstep GPT-2 + HIP-coder loop; RS + CRC framing; decode needs no state side channel."""
+    from neuralsteganography_amd.stego import stego_decode_batch, stego_encode_batch
+
+    _, lm = _tiny_provider()
+    msgs = [synthetic.payload_bytes(s, n) for s, n in enumerate((1, 40, 130, 0))]
+    q = {"temp": 1.0, "precision": 16, "topk": 300, "finish_sent": False}
+    res = stego_encode_batch(msgs, chunk_bytes=64, quality=q, seed_text="seed", lm=lm)
+    assert [r.metadata.total for r in res] == [1, 1, 3, 1]
+    lm.load_states([])  # decode must not depend on the bit-count side channel
+    assert stego_decode_batch([list(r) for r in res], quality=q, seed_text="seed", lm=lm) == msgs
