@@ -152,6 +152,38 @@ int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_
                    double temp, int topk, const int32_t* banned, int nbanned, double* d_stats,
                    ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
 
+/* Quality policies of the src rank coder (src/neuralstego/codec/quality.py:57-141 apply_quality /
+ * cap_bits_per_token, keys as codec/arithmetic.py:345-362 reads them).  Off: top_k <= 0, cap_bits <= 0,
+ * top_p <= 0, min_prob < 0. */
+typedef struct ns_rank_quality {
+    int32_t top_k;
+    int32_t cap_bits;
+    double top_p;
+    double min_prob;
+} ns_rank_quality;
+
+/* One step of the src package's own coder, the uniform rank coder of encode_with_lm
+ * (src/neuralstego/codec/arithmetic.py:122-168) over the softmax of logits/temp (lm/arithmetic.py:45-74): the
+ * n tokens left with nonzero probability by the quality policies are ranked (value desc, id asc), c =
+ * floor(log2 n) payload bits (read MSB-first per payload byte, zero padded) select the token of that rank.
+ * d_payload holds the packet BYTES (the api bit list packed LSB-first, i.e. the bytes themselves),
+ * d_payload_nbits their bit count; d_consumed_hist [B, hist_stride] receives the bits each token actually
+ * consumed (the reference's state["history"]).  No ids are banned on this path.  NS_ST_ERR_RANGE: no capacity
+ * (n < 2).  Runs on the wide path (every id sorted per step). */
+int ns_rank_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const uint8_t* d_payload,
+                        int64_t payload_stride, const int64_t* d_payload_nbits, ns_stream_state* d_state,
+                        int32_t* d_out_token, int32_t* d_token_hist, int32_t* d_consumed_hist, int64_t hist_stride,
+                        double temp, const ns_rank_quality* quality, ns_step_trace* d_trace, uint32_t step_flags,
+                        void* hip_stream);
+
+/* Decode step of the rank coder (codec/arithmetic.py:171-231): the received token's rank among the first 2^c,
+ * the first d_keep_bits[b] of its c bits (the consumption history) appended MSB-first into d_out_bits bytes.
+ * A token outside the first 2^c ranks: NS_ST_ERR_DIVERGE. */
+int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const int32_t* d_in_token,
+                        const int32_t* d_keep_bits, const uint8_t* d_active, ns_stream_state* d_state,
+                        uint8_t* d_out_bits, int64_t out_stride, double temp, const ns_rank_quality* quality,
+                        ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
+
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
  * (row re-read), counters[3] = top-K selections that left the histogram fast path (value ties or a skewed

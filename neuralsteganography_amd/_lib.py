@@ -27,6 +27,7 @@ NS_MAX_BANNED = 8
 
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
+           "ns_rank_encode_step", "ns_rank_decode_step",
            "ns_read_counters")
 
 
@@ -48,6 +49,13 @@ _lib = None
 
 class NativeLibraryError(RuntimeError):
     """The HIP coder library is missing or unusable (never silently replaced by a CPU path)."""
+
+
+class NsRankQuality(ctypes.Structure):
+    """``ns_rank_quality`` (include/nsg_coder.h)."""
+
+    _fields_ = [("top_k", ctypes.c_int32), ("cap_bits", ctypes.c_int32), ("top_p", ctypes.c_double),
+                ("min_prob", ctypes.c_double)]
 
 
 def lib() -> ctypes.CDLL:
@@ -83,6 +91,13 @@ def lib() -> ctypes.CDLL:
                                  ctypes.c_double, ctypes.c_int, i32p, ctypes.c_int, vp, ctypes.c_uint32, vp]
     L.ns_set_sentence_end.restype = ctypes.c_int
     L.ns_set_sentence_end.argtypes = [vp, vp]
+    L.ns_rank_encode_step.restype = ctypes.c_int
+    L.ns_rank_encode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, ctypes.c_int64, vp, vp, vp, vp, vp,
+                                      ctypes.c_int64, ctypes.c_double, ctypes.POINTER(NsRankQuality), vp,
+                                      ctypes.c_uint32, vp]
+    L.ns_rank_decode_step.restype = ctypes.c_int
+    L.ns_rank_decode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int64,
+                                      ctypes.c_double, ctypes.POINTER(NsRankQuality), vp, ctypes.c_uint32, vp]
     L.ns_set_rank_export.restype = ctypes.c_int
     L.ns_set_rank_export.argtypes = [vp, vp, ctypes.c_int]
     L.ns_set_stats.restype = ctypes.c_int

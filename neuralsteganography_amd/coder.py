@@ -532,3 +532,138 @@ class StreamingDecodeSession:
         ob = self.out_bits.cpu().numpy()
         return [np.unpackbits(ob[i], bitorder="little")[: int(f["bit_pos"][i])].astype(np.int64).tolist()
                 for i in range(self.B)]
+
+
+def rank_quality(quality) -> "_lib.NsRankQuality":
+    """src codec quality (``lm/arithmetic.py:77-95`` ``_normalise_quality``: topk/top_k, top_p, min_prob,
+    cap_per_token_bits / cap_bits_per_token) -> ``ns_rank_quality``."""
+    q = {}
+    for key, value in dict(quality or {}).items():
+        if value is None:
+            continue
+        k = key.replace("-", "_").lower()
+        if k in ("topk", "top_k"):
+            q["top_k"] = int(value)
+        elif k in ("topp", "top_p"):
+            q["top_p"] = float(value)
+        elif k in ("minprob", "min_prob"):
+            q["min_prob"] = float(value)
+        elif k in ("cap_per_token_bits", "cap_bits_per_token"):
+            q["cap"] = int(value)
+    if "top_k" in q and q["top_k"] <= 0:
+        raise ConfigurationError("top_k must be positive")
+    if "top_p" in q and not 0 < q["top_p"] <= 1:
+        raise ConfigurationError("top_p must be within (0, 1]")
+    if "min_prob" in q and q["min_prob"] < 0:
+        raise ConfigurationError("min_prob must be non-negative")
+    if "cap" in q and q["cap"] <= 0:
+        raise ConfigurationError("cap_per_token_bits must be positive")
+    return _lib.NsRankQuality(q.get("top_k", 0), q.get("cap", 0), q.get("top_p", 0.0), q.get("min_prob", -1.0))
+
+
+class RankEncodeSession:
+    """B payloads (bytes) encoded by the src rank coder (``codec/arithmetic.py:122-168``), one launch per
+    token; :meth:`consumed` is the reference's ``state["history"]`` per stream."""
+
+    def __init__(self, ctx: CoderContext, payloads: Sequence[bytes], *, temp: float, quality=None,
+                 max_tokens: Optional[int] = None):
+        torch = _torch()
+        self.ctx, self.B = ctx, len(payloads)
+        if self.B < 1 or self.B > ctx.max_batch:
+            raise ConfigurationError(f"batch {self.B} outside [1, {ctx.max_batch}]")
+        dev = torch.device("cuda", ctx.device)
+        self.temp, self.q = float(temp), rank_quality(quality)
+        self.nbytes = [len(bytes(pl)) for pl in payloads]
+        stride = max(1, max(self.nbytes))
+        buf = np.zeros((self.B, stride), dtype=np.uint8)
+        for i, pl in enumerate(payloads):
+            buf[i, : len(pl)] = np.frombuffer(bytes(pl), dtype=np.uint8)
+        self.payload = torch.from_numpy(buf).to(dev)
+        self.nbits = torch.tensor([8 * n for n in self.nbytes], dtype=torch.int64, device=dev)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        cap = max_tokens if max_tokens is not None else 8 * stride + 16
+        self.out_token = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.hist = torch.full((self.B, cap), -1, dtype=torch.int32, device=dev)
+        self.cons = torch.zeros((self.B, cap), dtype=torch.int32, device=dev)
+
+    def step(self, logits):
+        rc = _lib.lib().ns_rank_encode_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
+            _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), _ptr(self.cons),
+            self.hist.shape[1], self.temp, ctypes.byref(self.q), ctypes.c_void_p(0), 0, _stream_handle())
+        self.ctx.check(rc, "ns_rank_encode_step")
+        return self.out_token
+
+    def fields(self) -> dict:
+        return _state_fields(self.state)
+
+    def all_done(self) -> bool:
+        f = self.fields()
+        return bool(np.all((f["flags"] & _lib.NS_ST_DONE) != 0))
+
+    def raise_errors(self) -> None:
+        bad = np.nonzero(self.fields()["flags"] & _lib.NS_ST_ERR_RANGE)[0]
+        if bad.size:
+            raise ArithmeticRangeError(f"streams {bad.tolist()[:8]}: language model distribution provides no capacity")
+
+    def tokens(self) -> List[List[int]]:
+        self.raise_errors()
+        n = self.fields()["ntokens"]
+        h = self.hist.cpu().numpy()
+        return [h[i, : int(n[i])].astype(np.int64).tolist() for i in range(self.B)]
+
+    def consumed(self) -> List[List[int]]:
+        n = self.fields()["ntokens"]
+        c = self.cons.cpu().numpy()
+        return [c[i, : int(n[i])].astype(np.int64).tolist() for i in range(self.B)]
+
+
+class RankDecodeSession:
+    """Decode of the rank coder (``codec/arithmetic.py:171-231``) given every stream's consumption history."""
+
+    def __init__(self, ctx: CoderContext, token_lists: Sequence[Sequence[int]], histories: Sequence[Sequence[int]],
+                 *, temp: float, quality=None):
+        torch = _torch()
+        self.ctx, self.B = ctx, len(token_lists)
+        if self.B < 1 or self.B > ctx.max_batch:
+            raise ConfigurationError(f"batch {self.B} outside [1, {ctx.max_batch}]")
+        for tl, hs in zip(token_lists, histories):
+            if len(hs) < len(tl):
+                raise DecodeDivergenceError("Bit consumption history is required for decoding")
+        dev = torch.device("cuda", ctx.device)
+        self.temp, self.q = float(temp), rank_quality(quality)
+        self.T = max((len(t) for t in token_lists), default=0)
+        T1 = max(self.T, 1)
+        tok = np.zeros((T1, self.B), np.int32)
+        keep = np.zeros((T1, self.B), np.int32)
+        act = np.zeros((T1, self.B), np.uint8)
+        for i, (tl, hs) in enumerate(zip(token_lists, histories)):
+            n = len(tl)
+            tok[:n, i] = np.asarray(tl, np.int32)
+            keep[:n, i] = np.asarray(list(hs)[:n], np.int32)
+            act[:n, i] = 1
+        self.tok, self.keep, self.act = (torch.from_numpy(a).to(dev) for a in (tok, keep, act))
+        total = int(max((sum(list(h)[: len(t)]) for t, h in zip(token_lists, histories)), default=0))
+        self.out_stride = (total + 7) // 8 + 8
+        self.out_bits = torch.zeros((self.B, self.out_stride), dtype=torch.uint8, device=dev)
+        self.state = _state_tensor(self.B, dev)
+        ctx.check(_lib.lib().ns_init_state(ctx._h, _ptr(self.state), self.B, _stream_handle()), "ns_init_state")
+        self.t = 0
+
+    def step(self, logits) -> None:
+        t = self.t
+        rc = _lib.lib().ns_rank_decode_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok[t]), _ptr(self.keep[t]),
+            _ptr(self.act[t]), _ptr(self.state), _ptr(self.out_bits), self.out_stride, self.temp,
+            ctypes.byref(self.q), ctypes.c_void_p(0), 0, _stream_handle())
+        self.ctx.check(rc, "ns_rank_decode_step")
+        self.t += 1
+
+    def payloads(self) -> List[bytes]:
+        f = _state_fields(self.state)
+        bad = np.nonzero(f["flags"] & _lib.NS_ST_ERR_DIVERGE)[0]
+        if bad.size:
+            raise DecodeDivergenceError(f"streams {bad.tolist()[:8]}: token not present in distribution")
+        ob = self.out_bits.cpu().numpy()
+        return [ob[i, : int(f["bit_pos"][i]) // 8].tobytes() for i in range(self.B)]

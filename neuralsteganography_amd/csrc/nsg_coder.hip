@@ -1345,6 +1345,67 @@ int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_
     return NS_OK;
 }
 
+static int rank_prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_t ld, int B, double temp,
+                        const ns_rank_quality* q, ns_step_trace* d_trace, uint32_t flags, ns_stream_state* d_state) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
+    if (!q) return fail(ctx, NS_ERR_CONFIG, "rank step: null quality");
+    if (q->top_p > 1.0) return fail(ctx, NS_ERR_CONFIG, "top_p must be within (0, 1]");
+    if (ctx->vocab > 0x1FFFF) return fail(ctx, NS_ERR_UNSUPPORTED, "rank coder: vocab must be < 131072");
+    if (!ctx->wide.keys_in && nsg_wide_alloc(ctx) != NS_OK) {
+        nsg_wide_free(ctx);
+        return fail(ctx, NS_ERR_HIP, "rank coder: scratch allocation failed");
+    }
+    const int rc = prepare(ctx, p, d_logits, ld, B, temp, ctx->vocab, nullptr, 0, d_trace, flags, d_state);
+    if (rc != NS_OK) return rc;
+    p.rank = 1;
+    p.rk_top_k = q->top_k;
+    p.rk_cap = q->cap_bits;
+    p.rk_top_p = q->top_p;
+    p.rk_min_prob = q->min_prob;
+    return NS_OK;
+}
+
+int ns_rank_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const uint8_t* d_payload,
+                        int64_t payload_stride, const int64_t* d_payload_nbits, ns_stream_state* d_state,
+                        int32_t* d_out_token, int32_t* d_token_hist, int32_t* d_consumed_hist, int64_t hist_stride,
+                        double temp, const ns_rank_quality* quality, ns_step_trace* d_trace, uint32_t step_flags,
+                        void* hip_stream) {
+    nsg::StepParams p;
+    int rc = rank_prepare(ctx, p, d_logits, ld, B, temp, quality, d_trace, step_flags, d_state);
+    if (rc != NS_OK) return rc;
+    if (!d_payload || !d_payload_nbits || !d_out_token || payload_stride < 0)
+        return fail(ctx, NS_ERR_CONFIG, "ns_rank_encode_step: null payload/out pointer");
+    p.payload = d_payload;
+    p.payload_stride = payload_stride;
+    p.nbits = d_payload_nbits;
+    p.out_token = d_out_token;
+    p.hist = d_token_hist;
+    p.rk_cons = d_consumed_hist;
+    p.hist_stride = (d_token_hist || d_consumed_hist) ? hist_stride : 0;
+    if (!nsg_rank_launch(ctx, p, false, (hipStream_t)hip_stream))
+        return fail(ctx, NS_ERR_HIP, "ns_rank_encode_step: launch failed");
+    return NS_OK;
+}
+
+int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const int32_t* d_in_token,
+                        const int32_t* d_keep_bits, const uint8_t* d_active, ns_stream_state* d_state,
+                        uint8_t* d_out_bits, int64_t out_stride, double temp, const ns_rank_quality* quality,
+                        ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream) {
+    nsg::StepParams p;
+    int rc = rank_prepare(ctx, p, d_logits, ld, B, temp, quality, d_trace, step_flags, d_state);
+    if (rc != NS_OK) return rc;
+    if (!d_in_token || !d_keep_bits || !d_out_bits || out_stride < 1)
+        return fail(ctx, NS_ERR_CONFIG, "ns_rank_decode_step: null token/out pointer");
+    p.in_token = d_in_token;
+    p.rk_keep = d_keep_bits;
+    p.active = d_active;
+    p.out_bits = d_out_bits;
+    p.out_stride = out_stride;
+    if (!nsg_rank_launch(ctx, p, true, (hipStream_t)hip_stream))
+        return fail(ctx, NS_ERR_HIP, "ns_rank_decode_step: launch failed");
+    return NS_OK;
+}
+
 int ns_set_rank_export(ns_ctx* ctx, int32_t* d_ranked, int stride) {
     if (!ctx || (d_ranked && stride < 2)) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_export: bad argument");
     ctx->ranked = d_ranked;

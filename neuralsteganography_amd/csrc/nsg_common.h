@@ -182,6 +182,13 @@ struct StepParams {
     // decode: ranked ids of a diverged stream (ranks < k', then -1), [B][ranked_stride] (nullable)
     int32_t* ranked;
     int ranked_stride;
+    // src rank coder (ns_rank_encode_step / ns_rank_decode_step)
+    int rank;                 // 1: rank-coder step on the wide path
+    int rk_top_k, rk_cap;     // <= 0: off
+    double rk_top_p;          // <= 0: off
+    double rk_min_prob;       // < 0: off
+    int32_t* rk_cons;         // encode: bits consumed per token, [B][hist_stride]
+    const int32_t* rk_keep;   // decode: bits to keep this step, [B]
     // common
     ns_stream_state* state;
     ns_step_trace* trace;

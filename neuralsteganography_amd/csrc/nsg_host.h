@@ -58,3 +58,4 @@ struct ns_ctx {
 int nsg_wide_alloc(ns_ctx* ctx);  // NS_OK or NS_ERR_HIP
 void nsg_wide_free(ns_ctx* ctx);
 bool nsg_wide_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s);
+bool nsg_rank_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s);  // src rank coder

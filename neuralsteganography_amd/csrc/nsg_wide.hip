@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256) void wide_collect_kernel(StepParams p, const W
     const ns_stream_state st = p.state[b];
     const double thr = 1.0 / (double)(st.hi - st.lo);
     float xt;
-    if (p.sample) {
+    if (p.rank) {
+        xt = -__builtin_inff();  // the rank coder ranks every id
+    } else if (p.sample) {
         // sampler support e_i >= 2^-60  <=>  x >= m + temp * ln(2^-60); widened (extra ids are harmless)
         const double temp = 1.0 / p.inv_temp;
         const double t = (double)w.m - temp * 41.58883083359672;
@@ -599,6 +601,196 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     if (p.counters && exact) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1))], 1ull);
 }
 
+// ------------------------------------------------------------------------------------------ rank coder
+// src/neuralstego/codec/arithmetic.py:122-231 (encode_with_lm / decode_with_lm) with apply_quality /
+// cap_bits_per_token (codec/quality.py:57-141) over the _ModelAdapter softmax (lm/arithmetic.py:45-74):
+// canonical steps R1-R4 of oracle/nsg_oracle.c.  keys_sorted holds every id of the row in rank order.
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, const WideStat* ws,
+                                                                 const uint64_t* keys_sorted,
+                                                                 const unsigned int* count, int cap) {
+    __shared__ double ebuf[WIDE_ROUND];
+    __shared__ double sm64[64];
+    __shared__ int smi[16];
+    __shared__ int cut_sh;
+    __shared__ double acc_sh;
+    const int b = blockIdx.x;
+    const WideStat w = ws[b];
+    if (!w.active) return;
+    const int tid = threadIdx.x;
+    const ns_stream_state st = p.state[b];
+    const uint64_t* sk = keys_sorted + (int64_t)b * cap;
+    const int V = (int)count[b];
+    const double temp = 1.0 / p.inv_temp;
+    const double zmax = (double)wkey_val(sk[0]) / temp;
+    auto e_of = [&](int i) -> double { return exp_canon((double)wkey_val(sk[i]) / temp - zmax); };
+
+    // R1: S in the canonical rank order, p_i = e_i / S, n0 = #nonzero (a prefix)
+    double acc = 0.0;
+    for (int base = 0; base < V; base += WIDE_ROUND) {
+        for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? e_of(base + i) : 0.0;
+        __syncthreads();
+        if (tid < 64)
+            for (int i = tid; i < WIDE_ROUND && base + i < V; i += 64) acc += ebuf[i];
+        __syncthreads();
+    }
+    if (tid < 64) sm64[tid] = acc;
+    __syncthreads();
+    const double S = block_canonical_butterfly(sm64);
+    auto p_of = [&](int i) -> double { return e_of(i) / S; };
+    int fz = V;
+    for (int i = tid; i < V; i += WIDE_THREADS)
+        if (i < fz && e_of(i) == 0.0) fz = i;
+    int n = block_min_int(fz, smi);
+
+    // R2: top_k, top_p (left-to-right cumsum, searchsorted 'left'), min_prob
+    if (p.rk_top_k > 0) n = min(n, p.rk_top_k);
+    if (p.rk_top_p > 0.0) {
+        if (tid == 0) {
+            cut_sh = V;
+            acc_sh = 0.0;
+        }
+        __syncthreads();
+        for (int base = 0; base < V; base += WIDE_ROUND) {
+            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? p_of(base + i) : 0.0;
+            __syncthreads();
+            if (tid == 0 && cut_sh == V) {
+                double a = acc_sh;
+                for (int i = 0; i < WIDE_ROUND && base + i < V; ++i) {
+                    a += ebuf[i];
+                    if (a >= p.rk_top_p) {
+                        cut_sh = base + i;
+                        break;
+                    }
+                }
+                acc_sh = a;
+            }
+            __syncthreads();
+            if (cut_sh != V) break;
+        }
+        n = min(n, min(cut_sh + 1, V));
+    }
+    if (p.rk_min_prob >= 0.0) {
+        int fm = V;
+        for (int i = tid; i < V; i += WIDE_THREADS)
+            if (i < fm && !(p_of(i) >= p.rk_min_prob)) fm = i;
+        n = min(n, block_min_int(fm, smi));
+    }
+    // R3: cap_per_token_bits -- entropy of the renormalised support; bisect tau on softmax(log(f+1e-12)/tau)
+    // over every id (float64, libm-equivalent log/exp: tolerance-level)
+    if (p.rk_cap > 0 && n > 0) {
+        double fl = 0.0;
+        for (int i = tid; i < n; i += WIDE_THREADS) fl += p_of(i);
+        const double F = block_sum(fl, sm64);
+        double hl = 0.0;
+        for (int i = tid; i < n; i += WIDE_THREADS) {
+            const double f = p_of(i) / F;
+            if (f > 0.0) hl -= f * log2(f);
+        }
+        const double H = block_sum(hl, sm64);
+        if (H > (double)p.rk_cap) {
+            const double lf0 = log(p_of(0) / F + 1e-12);
+            double low = 1e-6, high = 1.0;
+            int n_target = n;
+            for (int it = 0; it < 60; ++it) {
+                const double mid = (low + high) / 2.0;
+                const double mx = lf0 / mid;
+                double sl = 0.0, tl = 0.0;
+                int zl = V;
+                for (int i = tid; i < V; i += WIDE_THREADS) {
+                    const double f = i < n ? p_of(i) / F : 0.0;
+                    const double a = log(f + 1e-12) / mid - mx;
+                    const double c = exp(a);
+                    if (c > 0.0) {
+                        sl += c;
+                        tl += c * a;
+                    } else if (i < zl) {
+                        zl = i;
+                    }
+                }
+                const double s = block_sum(sl, sm64);
+                const double t = block_sum(tl, sm64);
+                const int nz = block_min_int(zl, smi);
+                const double Hc = (log(s) - t / s) / 0.6931471805599453;  // entropy of c/s in bits
+                if (Hc > (double)p.rk_cap) {
+                    high = mid;
+                } else {
+                    low = mid;
+                    n_target = nz;
+                }
+            }
+            n = n_target;
+        }
+    }
+    // R4: capacity, selection
+    int c = 0;
+    while (c < 30 && (1 << (c + 1)) <= n) ++c;
+    if (c <= 0) {
+        if (tid == 0) p.state[b].flags = st.flags | (DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE) | NS_ST_DONE;
+        return;
+    }
+    if (!DECODE) {
+        if (tid != 0) return;
+        const int64_t nbits = p.nbits[b];
+        const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
+        uint32_t idx = 0;
+        int take = 0;
+        for (int t = 0; t < c; ++t) {
+            const int64_t bp = st.bit_pos + t;
+            uint32_t bit = 0;
+            if (bp < nbits) {
+                bit = (pl[bp >> 3] >> (7 - (bp & 7))) & 1u;
+                ++take;
+            }
+            idx = (idx << 1) | bit;
+        }
+        const int32_t token = (int32_t)wkey_id(sk[idx]);
+        ns_stream_state ns = st;
+        ns.bit_pos = st.bit_pos + take;
+        ns.ntokens = st.ntokens + 1;
+        if (ns.bit_pos >= nbits) ns.flags |= NS_ST_DONE;
+        p.state[b] = ns;
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        if (p.rk_cons && st.ntokens < p.hist_stride) p.rk_cons[(int64_t)b * p.hist_stride + st.ntokens] = take;
+        if (p.trace) {
+            ns_step_trace tr = {n, c, (int)idx, take, token, 0, S};
+            p.trace[b] = tr;
+        }
+        return;
+    }
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const int32_t tok = p.in_token[b];
+    int found = 0x7FFFFFFF;
+    if (tok >= 0 && tok < p.V) {
+        const uint64_t kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+        for (int i = tid; i < (1 << c); i += WIDE_THREADS)
+            if (sk[i] == kt) found = i;
+    }
+    const int idx = block_min_int(found, smi);
+    if (tid != 0) return;
+    if (idx == 0x7FFFFFFF) {
+        p.state[b].flags = st.flags | NS_ST_ERR_DIVERGE | NS_ST_DONE;
+        return;
+    }
+    const int keep = min(max(p.rk_keep[b], 0), c);
+    uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
+    for (int t = 0; t < keep; ++t) {
+        const int64_t bp = st.bit_pos + t;
+        const uint8_t bitv = (uint8_t)((idx >> (c - 1 - t)) & 1);
+        const uint8_t m = (uint8_t)(0x80u >> (bp & 7));
+        ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | m) : (uint8_t)(ob[bp >> 3] & ~m);
+    }
+    ns_stream_state ns = st;
+    ns.bit_pos = st.bit_pos + keep;
+    ns.ntokens = st.ntokens + 1;
+    p.state[b] = ns;
+    if (p.trace) {
+        ns_step_trace tr = {n, c, idx, keep, tok, 0, S};
+        p.trace[b] = tr;
+    }
+}
+
 }  // namespace nsg
 
 // ------------------------------------------------------------------------------------------ host
@@ -650,6 +842,33 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B), dim3(nsg::WIDE_THREADS), 0, s, p, w.stat,
                        w.keys_out, w.count, w.cap);
     return hipGetLastError() == hipSuccess;
+}
+
+template <typename T, bool DECODE>
+static bool rank_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
+    NsgWide& w = ctx->wide;
+    const int B = p.B;
+    hipLaunchKernelGGL((nsg::wide_stats_kernel<T, DECODE>), dim3((B + nsg::WPB - 1) / nsg::WPB),
+                       dim3(nsg::WPB * nsg::WAVE), 0, s, p, w.stat, w.count);
+    const int nchunk = (p.V + nsg::COLLECT_CHUNK - 1) / nsg::COLLECT_CHUNK;
+    hipLaunchKernelGGL((nsg::wide_collect_kernel<T>), dim3(nchunk, B), dim3(256), 0, s, p, w.stat, w.keys_in,
+                       w.count, w.cap);
+    hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
+                       w.count, w.begin, w.end);
+    size_t bytes = w.sort_tmp_bytes;
+    if (rocprim::segmented_radix_sort_keys_desc(w.sort_tmp, bytes, w.keys_in, w.keys_out,
+                                                (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin,
+                                                w.end, 0, 49, s) != hipSuccess)
+        return false;
+    hipLaunchKernelGGL((nsg::wide_rank_kernel<T, DECODE>), dim3(B), dim3(nsg::WIDE_THREADS), 0, s, p, w.stat,
+                       w.keys_out, w.count, w.cap);
+    return hipGetLastError() == hipSuccess;
+}
+
+bool nsg_rank_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s) {
+    if (ctx->dtype == NS_DTYPE_F16)
+        return decode ? rank_launch_t<_Float16, true>(ctx, p, s) : rank_launch_t<_Float16, false>(ctx, p, s);
+    return decode ? rank_launch_t<float, true>(ctx, p, s) : rank_launch_t<float, false>(ctx, p, s);
 }
 
 bool nsg_wide_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s) {

@@ -71,6 +71,8 @@ class ByteTokenizer:
 class HipArithmeticLM:
     """Arithmetic-coding provider: batched GPT-2 on PyTorch-ROCm + the HIP coder step."""
 
+    decodes_without_state = True  # the interval coder needs no per-token history (unlike the rank coder)
+
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
                  compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096):
         import torch

@@ -1,0 +1,184 @@
+"""``HipRankLM``: the src package's own provider (``src/neuralstego/lm/arithmetic.py:115-264``, ``ArithmeticLM``)
+on the GPU -- the uniform rank coder of ``codec/arithmetic.py:122-231`` (``encode_with_lm`` /
+``decode_with_lm``) with its quality policies, over a KV-cached batched GPT-2 and the HIP rank kernel.
+
+Same protocol and side channel as the reference: ``encode_arithmetic`` returns token ids and queues a
+``{"history", "residual_bits"}`` state (bits consumed per token, payload bit count); ``decode_arithmetic``
+pops one and needs it (the rank coder cannot decode without the history, ``codec/arithmetic.py:188-189``).
+Quality keys follow ``lm/arithmetic.py:77-112``: temp / temperature, topk / top_k, top_p, min_prob,
+cap_per_token_bits, max_context.
+
+Deviation: the reference re-runs the whole (trimmed) context per token; this provider keeps a KV cache with
+positions modulo ``n_positions`` -- identical logits while the context fits ``n_positions`` (and no
+``max_context`` trimming is requested), which covers the api's packet-sized streams.
+"""
+
+from __future__ import annotations
+
+from collections import deque
+from typing import Deque, Dict, Iterable, List, Mapping, Optional, Sequence
+
+from ..coder import CoderContext, CoderParams, RankDecodeSession, RankEncodeSession
+from ..exceptions import ConfigurationError
+from .arithmetic import ByteTokenizer
+
+CodecState = Dict[str, object]
+
+
+def _bits_to_bytes(bits: Sequence[int]) -> bytes:
+    if len(bits) % 8:
+        raise ConfigurationError("bit stream length must be a multiple of 8")
+    out = bytearray(len(bits) // 8)
+    for i in range(len(out)):
+        out[i] = sum((int(bits[8 * i + k]) & 1) << k for k in range(8))
+    return bytes(out)
+
+
+def _bytes_to_bits(data: bytes) -> List[int]:
+    return [(b >> k) & 1 for b in bytes(data) for k in range(8)]
+
+
+def _temperature(quality: Optional[Mapping[str, object]]) -> float:
+    for key in ("temp", "temperature"):
+        if quality and quality.get(key) is not None:
+            t = float(quality[key])
+            if t <= 0:
+                raise ConfigurationError("temperature must be positive")
+            return t
+    return 1.0
+
+
+class HipRankLM:
+    """Rank-coder provider: batched GPT-2 (or any ``prefill``/``step`` batched LM) + the HIP rank kernel."""
+
+    def __init__(self, model=None, tokenizer=None, *, batched_lm=None, device: Optional[str] = None,
+                 logits_dtype: str = "f32", compute_dtype=None, max_batch: int = 4096):
+        import torch
+
+        if not torch.cuda.is_available():
+            from .._lib import NativeLibraryError
+
+            raise NativeLibraryError("HipRankLM needs a ROCm GPU (the rank coder has no CPU path)")
+        if batched_lm is None:
+            from .gpt2 import BatchedGPT2
+
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            ldt = torch.float16 if logits_dtype == "f16" else torch.float32
+            batched_lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
+        self.lm = batched_lm
+        self.vocab = self.lm.shape.vocab
+        self.tokenizer = tokenizer if tokenizer is not None else ByteTokenizer(self.vocab)
+        self.logits_dtype = logits_dtype
+        self.max_batch = int(max_batch)
+        self.device_index = torch.cuda.current_device()
+        self._ctx: Dict[int, CoderContext] = {}
+        self._encode_states: List[CodecState] = []
+        self._decode_states: Deque[CodecState] = deque()
+
+    def _coder(self, B: int) -> CoderContext:
+        ctx = self._ctx.get(B)
+        if ctx is None:
+            params = CoderParams(vocab=self.vocab, precision=16, temp=1.0, topk=self.vocab, dtype=self.logits_dtype,
+                                 banned=[])
+            ctx = CoderContext(params, max_batch=B, device=self.device_index)
+            self._ctx[B] = ctx
+        return ctx
+
+    # ------------------------------------------------------------------ protocol (api.py:42-56)
+    def encode_seed(self, text: str) -> List[int]:
+        tok = self.tokenizer
+        try:
+            bos = list(tok.encode("<|endoftext|>", add_special_tokens=False))
+        except TypeError:
+            bos = list(tok.encode("<|endoftext|>"))
+        try:
+            body = list(tok.encode(text, add_special_tokens=False))
+        except TypeError:
+            body = list(tok.encode(text))
+        return [int(t) for t in bos + body]
+
+    def encode_arithmetic(self, bits: List[int], context: List[int], *, quality: Mapping[str, object]) -> List[int]:
+        return self.encode_batch([bits], context, quality=quality)[0]
+
+    def decode_arithmetic(self, tokens: List[int], context: List[int], *, quality: Mapping[str, object]) -> List[int]:
+        if not tokens:
+            if self._decode_states:
+                self._decode_states.popleft()
+            return []
+        if not self._decode_states:
+            raise ConfigurationError("decode state unavailable for the rank coder")
+        st = self._decode_states.popleft()
+        return self.decode_batch([tokens], context, quality=quality, states=[st])[0]
+
+    def drain_states(self) -> List[CodecState]:
+        out = [dict(s) for s in self._encode_states]
+        self._encode_states.clear()
+        return out
+
+    def load_states(self, states: Iterable[CodecState]) -> None:
+        self._decode_states = deque(dict(s) for s in states)
+
+    # ------------------------------------------------------------------ batched
+    def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                     quality: Mapping[str, object], max_steps: int = 1 << 16) -> List[List[int]]:
+        B = len(bit_lists)
+        if B == 0:
+            return []
+        payloads = [_bits_to_bytes(list(b)) for b in bit_lists]
+        empty = [len(p) == 0 for p in payloads]
+        ctx = self._coder(B)
+        sess = RankEncodeSession(ctx, [p if p else b"\x00" for p in payloads], temp=_temperature(quality),
+                                 quality=quality)
+        if any(empty):  # encode_with_lm returns no token for an empty payload (:150-154)
+            sess.nbits[[i for i, e in enumerate(empty) if e]] = 0
+        import torch
+
+        logits = self.lm.prefill(list(context)[-1022:] or [0], B, 8 * max(len(p) for p in payloads) + 2)
+        for t in range(max_steps):
+            if t % 8 == 0:
+                sess.raise_errors()
+                if sess.all_done():
+                    break
+            tok = sess.step(logits)
+            logits = self.lm.step(tok.to(torch.long))
+        toks, cons = sess.tokens(), sess.consumed()
+        for i in range(B):
+            if empty[i]:
+                toks[i], cons[i] = [], []
+            st = {"history": tuple(cons[i]), "residual_bits": (8 * len(payloads[i])).to_bytes(8, "big")}
+            self._encode_states.append(dict(st))
+            self._decode_states.append(dict(st))
+        return toks
+
+    def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                     quality: Mapping[str, object], states: Optional[Sequence[CodecState]] = None) -> List[List[int]]:
+        import torch
+
+        B = len(token_lists)
+        if B == 0:
+            return []
+        if states is None:
+            states = [self._decode_states.popleft() if self._decode_states else {} for _ in range(B)]
+        hist = [list(s.get("history") or ()) for s in states]
+        for tl in token_lists:
+            if any(not 0 <= int(t) < self.vocab for t in tl):
+                from ..codec.errors import DecodeDivergenceError
+
+                raise DecodeDivergenceError(f"token id outside [0, {self.vocab})")
+        ctx = self._coder(B)
+        sess = RankDecodeSession(ctx, token_lists, hist, temp=_temperature(quality), quality=quality)
+        logits = self.lm.prefill(list(context)[-1022:] or [0], B, max(sess.T, 1) + 1)
+        for t in range(sess.T):
+            sess.step(logits)
+            if t + 1 < sess.T:
+                logits = self.lm.step(sess.tok[t].to(torch.long))
+        out = []
+        for i, pl in enumerate(sess.payloads()):
+            nb = states[i].get("residual_bits")
+            if nb:
+                pl = pl[: int.from_bytes(bytes(nb), "big") // 8]
+            out.append(_bytes_to_bits(pl))
+        return out
+
+
+__all__ = ["HipRankLM"]

@@ -102,10 +102,13 @@ def _encode_streams(lm, bit_lists: List[List[int]], context: List[int], quality:
 
 def _decode_streams(lm, spans: List[List[int]], context: List[int], quality: Dict[str, Any]) -> List[List[int]]:
     if hasattr(lm, "decode_batch"):
-        queue = getattr(lm, "_decode_states", None)
-        if queue:
-            for _ in range(min(len(spans), len(queue))):
-                queue.popleft()
+        if getattr(lm, "decodes_without_state", False):
+            # the arithmetic coder decodes from the tokens alone: drop the queued states to stay aligned
+            queue = getattr(lm, "_decode_states", None)
+            if queue:
+                for _ in range(min(len(spans), len(queue))):
+                    queue.popleft()
+        # (a provider that needs its history, like the rank coder, pops its own states in decode_batch)
         return lm.decode_batch(spans, context, quality=quality)
     return [lm.decode_arithmetic(list(span), context, quality=quality) for span in spans]
 

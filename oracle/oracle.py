@@ -29,6 +29,19 @@ class OrState(ctypes.Structure):
                 ("ntokens", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
+class OrRankQuality(ctypes.Structure):
+    _fields_ = [("top_k", ctypes.c_int32), ("top_p", ctypes.c_double), ("min_prob", ctypes.c_double),
+                ("cap_bits", ctypes.c_int32)]
+
+
+def rank_quality(quality) -> OrRankQuality:
+    """src codec quality keys (codec/arithmetic.py:345-362) -> the oracle struct (off = <=0 / <0)."""
+    q = dict(quality or {})
+    return OrRankQuality(int(q.get("top_k") or 0), float(q.get("top_p") or 0.0),
+                         float(q["min_prob"]) if q.get("min_prob") is not None else -1.0,
+                         int(q.get("cap_per_token_bits") or 0))
+
+
 class OrTrace(ctypes.Structure):
     _fields_ = [("k", ctypes.c_int32), ("kprime", ctypes.c_int32), ("sel", ctypes.c_int32),
                 ("n", ctypes.c_int32), ("token", ctypes.c_int32), ("pad", ctypes.c_int32),
@@ -79,6 +92,10 @@ def lib() -> ctypes.CDLL:
         L.or_sample_step.argtypes = [fp, ctypes.c_int, i32p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                      ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(OrState), i32p,
                                      ctypes.POINTER(OrTrace), dp]
+        L.or_rank_step.restype = ctypes.c_int
+        L.or_rank_step.argtypes = [fp, ctypes.c_int, ctypes.c_double, ctypes.POINTER(OrRankQuality), ctypes.c_int,
+                                   u8p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(OrState),
+                                   i32p, i32p, u8p, i32p]
         L.or_encode_batch.restype = ctypes.c_int
         L.or_encode_batch.argtypes = [fp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, i32p, ctypes.c_int,
                                       ctypes.c_double, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int64,
@@ -261,6 +278,43 @@ def sample_stats_for_tokens(row_fn: RowFn, tokens: Sequence[int], *, banned, tem
         acc[2] += -np.sum(np.where(q > 0, q * lq, 0.0)) / 0.69315
         acc[3] += 1
     return stats_summary(acc)
+
+
+def rank_encode_stream(row_fn: RowFn, payload: bytes, *, temp: float, quality) -> Tuple[List[int], List[int]]:
+    """src ``encode_with_lm`` (codec/arithmetic.py:122-168): tokens and the bits each consumed."""
+    pl = np.frombuffer(bytes(payload), dtype=np.uint8).copy() if payload else np.zeros(1, np.uint8)
+    nbits = 8 * len(payload)
+    rq = rank_quality(quality)
+    st = new_state(1)
+    toks, cons = [], []
+    t = 0
+    while st.bit_pos < nbits:
+        x = np.ascontiguousarray(row_fn(t), dtype=np.float32)
+        tok, c, cap = ctypes.c_int32(-1), ctypes.c_int32(0), ctypes.c_int32(0)
+        rc = lib().or_rank_step(_fptr(x), x.size, 1.0 / float(temp), ctypes.byref(rq), 0, _u8(pl), nbits, -1, 0,
+                                ctypes.byref(st), ctypes.byref(tok), ctypes.byref(c), None, ctypes.byref(cap))
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle rank encode step {t} failed rc={rc}")
+        toks.append(tok.value)
+        cons.append(c.value)
+        t += 1
+    return toks, cons
+
+
+def rank_decode_stream(row_fn: RowFn, tokens: Sequence[int], consumed: Sequence[int], nbits: int, *, temp: float,
+                       quality) -> bytes:
+    """src ``decode_with_lm`` (codec/arithmetic.py:171-231) given the consumption history."""
+    rq = rank_quality(quality)
+    st = new_state(1)
+    out = np.zeros(max(1, (sum(consumed) + 7) // 8 + 8), dtype=np.uint8)
+    for t, tok in enumerate(tokens):
+        x = np.ascontiguousarray(row_fn(t), dtype=np.float32)
+        cap = ctypes.c_int32(0)
+        rc = lib().or_rank_step(_fptr(x), x.size, 1.0 / float(temp), ctypes.byref(rq), 1, None, 0, int(tok),
+                                int(consumed[t]), ctypes.byref(st), None, None, _u8(out), ctypes.byref(cap))
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle rank decode step {t} failed rc={rc}")
+    return out.tobytes()[: nbits // 8]
 
 
 def decode_stream(row_fn: RowFn, tokens: Sequence[int], *, banned, temp: float, precision: int,

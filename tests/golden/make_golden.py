@@ -218,6 +218,64 @@ def run_sample_config(name, cfg, stable_sort_mode):
     return out
 
 
+# src rank coder (src/neuralstego/codec/arithmetic.py encode_with_lm / decode_with_lm) behind the src
+# ArithmeticLM's _ModelAdapter (lm/arithmetic.py:45-74: softmax of logits.double()/temp): name -> vocab,
+# logit scale, temperature, codec quality, payload bytes per stream.
+RANK_CONFIGS = {
+    "r1_v50257_k50000": dict(vocab=50257, scale=3.0, temp=1.0, quality={"top_k": 50000}, nbytes=[32, 9]),
+    "r2_v50257_k300": dict(vocab=50257, scale=3.0, temp=0.9, quality={"top_k": 300}, nbytes=[24, 5]),
+    "r3_v50257_p09": dict(vocab=50257, scale=3.0, temp=1.0, quality={"top_p": 0.9}, nbytes=[24]),
+    "r4_v50257_minp": dict(vocab=50257, scale=3.0, temp=1.0, quality={"min_prob": 1e-5}, nbytes=[24]),
+    "r5_v50257_k1000_cap6": dict(vocab=50257, scale=3.0, temp=1.0, quality={"top_k": 1000, "cap_per_token_bits": 6},
+                                 nbytes=[16]),
+    "r6_v700_k600_t07": dict(vocab=700, scale=2.0, temp=0.7, quality={"top_k": 600, "top_p": 0.95}, nbytes=[20, 3]),
+}
+
+
+class RowProvider:
+    """``next_token_probs`` of the src _ModelAdapter (lm/arithmetic.py:45-74) over synthetic rows: call t
+    returns softmax(float64(logits_row(t)) / temp) computed by torch, whatever the context."""
+
+    def __init__(self, seed, stream, vocab, scale, temp):
+        import torch
+
+        self.torch = torch
+        self.seed, self.stream, self.vocab, self.scale, self.temp = seed, stream, vocab, scale, temp
+        self.calls = 0
+
+    def next_token_probs(self, context_ids):
+        row = synthetic.logits_row(self.seed, self.stream, self.calls, self.vocab, self.scale, np.float32)
+        self.calls += 1
+        logits = self.torch.from_numpy(row.copy()).to(dtype=self.torch.float64) / self.temp
+        return self.torch.nn.functional.softmax(logits, dim=-1).numpy()
+
+
+def run_rank_config(name, cfg):
+    sys.path.insert(0, str(REF / "src"))
+    from neuralstego.codec import arithmetic as src_coder  # src/neuralstego/codec/arithmetic.py
+
+    assert Path(src_coder.__file__).resolve() == (REF / "src/neuralstego/codec/arithmetic.py").resolve()
+    out = {"tokens": [], "tok_off": [0], "cons": [], "payload": [], "pay_off": [0], "decoded": [], "dec_off": [0]}
+    for s, nbytes in enumerate(cfg["nbytes"]):
+        payload = synthetic.payload_bytes(s, nbytes)
+        state = {}
+        prov = RowProvider(LOGIT_SEED, s, cfg["vocab"], cfg["scale"], cfg["temp"])
+        toks = src_coder.encode_with_lm(payload, prov, context=synthetic.DEFAULT_CONTEXT, quality=cfg["quality"],
+                                        state=state)
+        dstate = dict(state)
+        dprov = RowProvider(LOGIT_SEED, s, cfg["vocab"], cfg["scale"], cfg["temp"])
+        dec = src_coder.decode_with_lm(toks, dprov, context=synthetic.DEFAULT_CONTEXT, quality=cfg["quality"],
+                                       state=dstate)
+        assert dec == payload, f"{name} stream {s}: reference round trip failed"
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["cons"] += list(state["history"])
+        out["payload"] += list(payload); out["pay_off"].append(len(out["payload"]))
+        out["decoded"] += list(dec); out["dec_off"].append(len(out["decoded"]))
+        print(f"  {name} s={s} bytes={nbytes} tokens={len(toks)} bits/token={8 * nbytes / max(1, len(toks)):.2f}",
+              flush=True)
+    return out
+
+
 def run_compat_config(name, cfg, ref, stable_sort_mode):
     from tests.golden.toy_tokenizer import ToyTokenizer
 
@@ -253,6 +311,20 @@ def run_compat_config(name, cfg, ref, stable_sort_mode):
 
 def main(names=None):
     ref, stable = _import_reference()
+    for name, cfg in RANK_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_rank_config(name, cfg)
+        meta = dict(cfg, name=name, kind="rank", logit_seed=LOGIT_SEED, payload_seed=synthetic.PAYLOAD_SEED,
+                    context=synthetic.DEFAULT_CONTEXT,
+                    reference="src/neuralstego/codec/arithmetic.py encode_with_lm / decode_with_lm")
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            consumed=np.asarray(res["cons"], dtype=np.int32),
+            payload=np.asarray(res["payload"], dtype=np.uint8), pay_off=np.asarray(res["pay_off"], np.int64),
+            decoded=np.asarray(res["decoded"], dtype=np.uint8), dec_off=np.asarray(res["dec_off"], np.int64))
     for name, cfg in COMPAT_CONFIGS.items():
         if names and name not in names:
             continue
