@@ -184,6 +184,13 @@ int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, co
                         uint8_t* d_out_bits, int64_t out_stride, double temp, const ns_rank_quality* quality,
                         ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
 
+/* next_token_probs of the src distribution providers (codec/distribution.py:107-142, lm/arithmetic.py:45-74):
+ * d_probs [B, probs_stride] float64 receives, by token id, softmax(logits / temp) restricted to the
+ * quality support (top_k / top_p / min_prob of `quality`, cap_bits ignored) and renormalised, zeros
+ * elsewhere.  d_scratch_state: [B] states the call may overwrite. */
+int ns_token_probs(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, double temp, const ns_rank_quality* quality,
+                   double* d_probs, int64_t probs_stride, ns_stream_state* d_scratch_state, void* hip_stream);
+
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
  * (row re-read), counters[3] = top-K selections that left the histogram fast path (value ties or a skewed

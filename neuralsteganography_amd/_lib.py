@@ -27,7 +27,7 @@ NS_MAX_BANNED = 8
 
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
-           "ns_rank_encode_step", "ns_rank_decode_step",
+           "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
            "ns_read_counters")
 
 
@@ -98,6 +98,9 @@ def lib() -> ctypes.CDLL:
     L.ns_rank_decode_step.restype = ctypes.c_int
     L.ns_rank_decode_step.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int64,
                                       ctypes.c_double, ctypes.POINTER(NsRankQuality), vp, ctypes.c_uint32, vp]
+    L.ns_token_probs.restype = ctypes.c_int
+    L.ns_token_probs.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                 ctypes.POINTER(NsRankQuality), vp, ctypes.c_int64, vp, vp]
     L.ns_set_rank_export.restype = ctypes.c_int
     L.ns_set_rank_export.argtypes = [vp, vp, ctypes.c_int]
     L.ns_set_stats.restype = ctypes.c_int

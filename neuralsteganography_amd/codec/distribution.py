@@ -1,0 +1,124 @@
+"""``next_token_probs`` providers (``src/neuralstego/codec/distribution.py``; a15 of SURVEY §8).
+
+* :class:`HipTransformersLM` -- ``TransformersLM.next_token_probs`` (``:107-142``) on the GPU: GPT-2 logits of
+  the context (KV cache kept and extended when the next query appends one token, instead of the
+  reference's full re-forward per query), float64 softmax of ``logits / temperature`` and the
+  ``top_k`` / ``top_p`` / ``min_prob`` support renormalised, computed by the HIP rank kernel
+  (``ns_token_probs``).
+* :class:`MockLM` -- the fixed Zipf distribution of ``:17-37`` (host).
+* :class:`CachedLM` -- the LRU memo of ``:40-60`` (host).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .. import _lib
+from ..exceptions import ConfigurationError
+
+
+class MockLM:
+    """Context-free Zipf prior: p(rank r) proportional to r^-alpha over ``vocab_size`` ids."""
+
+    def __init__(self, vocab_size: int = 32, alpha: float = 1.2):
+        if vocab_size <= 0:
+            raise ValueError("vocab_size must be positive")
+        if alpha <= 0:
+            raise ValueError("alpha must be positive")
+        w = np.arange(1, vocab_size + 1, dtype=np.float64) ** -float(alpha)
+        self.vocab_size, self.alpha = int(vocab_size), float(alpha)
+        self._p = w / w.sum()
+
+    def next_token_probs(self, context_ids: Sequence[int]) -> np.ndarray:
+        del context_ids
+        return self._p.copy()
+
+
+class CachedLM:
+    """Memoise ``next_token_probs`` per context tuple (least recently used eviction beyond ``maxsize``)."""
+
+    def __init__(self, lm, *, maxsize: int = 128):
+        if maxsize <= 0:
+            raise ValueError("maxsize must be positive")
+        self._lm, self._maxsize = lm, int(maxsize)
+        self._memo: "OrderedDict[tuple, object]" = OrderedDict()
+
+    def next_token_probs(self, context_ids: Sequence[int]):
+        key = tuple(int(t) for t in context_ids)
+        if key in self._memo:
+            self._memo.move_to_end(key)
+        else:
+            self._memo[key] = self._lm.next_token_probs(list(key))
+            while len(self._memo) > self._maxsize:
+                self._memo.popitem(last=False)
+        val = self._memo[key]
+        return dict(val) if isinstance(val, dict) else np.array(val, copy=True)
+
+
+class HipTransformersLM:
+    """GPU ``next_token_probs`` over a batched GPT-2 (or any ``prefill``/``step`` batched LM)."""
+
+    def __init__(self, model=None, *, batched_lm=None, temperature: float = 1.0, top_k: Optional[int] = None,
+                 top_p: Optional[float] = None, min_prob: Optional[float] = None, max_context: Optional[int] = None,
+                 logits_dtype: str = "f32", tokenizer=None):
+        import torch
+
+        from ..coder import CoderContext, CoderParams, rank_quality
+
+        if temperature <= 0.0:
+            raise ValueError("temperature must be positive")
+        if not torch.cuda.is_available():
+            raise _lib.NativeLibraryError("HipTransformersLM needs a ROCm GPU")
+        if batched_lm is None:
+            from ..lm.gpt2 import BatchedGPT2
+
+            ldt = torch.float16 if logits_dtype == "f16" else torch.float32
+            batched_lm = BatchedGPT2(model, device=torch.device("cuda", torch.cuda.current_device()), logits_dtype=ldt)
+        self.lm, self.tokenizer = batched_lm, tokenizer
+        self.vocab = self.lm.shape.vocab
+        self.temperature = float(temperature)
+        self.max_context = max_context
+        self._q = rank_quality({"top_k": top_k, "top_p": top_p, "min_prob": min_prob})
+        params = CoderParams(vocab=self.vocab, precision=16, temp=1.0, topk=self.vocab, dtype=logits_dtype, banned=[])
+        self._ctx = CoderContext(params, max_batch=1)
+        dev = torch.device("cuda", self._ctx.device)
+        self._probs = torch.zeros((1, self.vocab), dtype=torch.float64, device=dev)
+        self._state = torch.zeros((1, 4), dtype=torch.int64, device=dev)
+        self._last: Optional[tuple] = None
+        self._logits = None
+
+    def _window(self) -> Optional[int]:
+        if self.max_context is not None and self.max_context > 0:
+            return int(self.max_context)
+        return int(getattr(self.lm.shape, "n_positions", 0)) or None
+
+    def next_token_probs(self, context_ids: Sequence[int]) -> np.ndarray:
+        import torch
+
+        from ..coder import _ptr, _stream_handle
+
+        ctx = tuple(int(t) for t in context_ids)
+        if not ctx:
+            raise ValueError("context_ids must contain at least one token")
+        win = self._window()
+        if win is not None and len(ctx) > win:
+            ctx = ctx[-win:]
+            self._last = None  # a sliding window changes every position: recompute
+        if self._last is not None and len(ctx) == len(self._last) + 1 and ctx[:-1] == self._last:
+            self._logits = self.lm.step(torch.tensor([ctx[-1]], device=self._probs.device, dtype=torch.long))
+        else:
+            self._logits = self.lm.prefill(list(ctx), 1, 64)
+        self._last = ctx
+        lg = self._logits
+        rc = _lib.lib().ns_token_probs(self._ctx._h, _ptr(lg), lg.stride(0), 1, self.temperature,
+                                       ctypes.byref(self._q), _ptr(self._probs), self._probs.stride(0),
+                                       _ptr(self._state), _stream_handle())
+        self._ctx.check(rc, "ns_token_probs")
+        return self._probs[0].cpu().numpy().copy()
+
+
+__all__ = ["MockLM", "CachedLM", "HipTransformersLM"]

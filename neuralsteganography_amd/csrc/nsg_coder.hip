@@ -1406,6 +1406,21 @@ int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, co
     return NS_OK;
 }
 
+int ns_token_probs(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, double temp, const ns_rank_quality* quality,
+                   double* d_probs, int64_t probs_stride, ns_stream_state* d_scratch_state, void* hip_stream) {
+    nsg::StepParams p;
+    int rc = rank_prepare(ctx, p, d_logits, ld, B, temp, quality, nullptr, 0, d_scratch_state);
+    if (rc != NS_OK) return rc;
+    if (!d_probs || probs_stride < ctx->vocab) return fail(ctx, NS_ERR_CONFIG, "ns_token_probs: bad output");
+    p.probs_out = d_probs;
+    p.probs_stride = probs_stride;
+    hipLaunchKernelGGL(nsg::init_state_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream,
+                       d_scratch_state, B, ctx->precision);
+    if (!nsg_rank_launch(ctx, p, true, (hipStream_t)hip_stream))
+        return fail(ctx, NS_ERR_HIP, "ns_token_probs: launch failed");
+    return NS_OK;
+}
+
 int ns_set_rank_export(ns_ctx* ctx, int32_t* d_ranked, int stride) {
     if (!ctx || (d_ranked && stride < 2)) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_export: bad argument");
     ctx->ranked = d_ranked;

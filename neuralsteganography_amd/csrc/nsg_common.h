@@ -189,6 +189,8 @@ struct StepParams {
     double rk_min_prob;       // < 0: off
     int32_t* rk_cons;         // encode: bits consumed per token, [B][hist_stride]
     const int32_t* rk_keep;   // decode: bits to keep this step, [B]
+    double* probs_out;        // ns_token_probs: filtered, renormalised p by id, [B][probs_stride]
+    int64_t probs_stride;
     // common
     ns_stream_state* state;
     ns_step_trace* trace;

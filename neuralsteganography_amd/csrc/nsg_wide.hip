@@ -676,6 +676,19 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
             if (i < fm && !(p_of(i) >= p.rk_min_prob)) fm = i;
         n = min(n, block_min_int(fm, smi));
     }
+    // next_token_probs (codec/distribution.py:107-142): the quality-filtered support renormalised, by id
+    if (p.probs_out) {
+        const bool filtered = p.rk_top_k > 0 || p.rk_top_p > 0.0 || p.rk_min_prob >= 0.0;
+        const int keep = filtered ? n : V;
+        double fl = 0.0;
+        for (int i = tid; i < keep; i += WIDE_THREADS) fl += p_of(i);
+        const double F = block_sum(fl, sm64);
+        double* out = p.probs_out + (int64_t)b * p.probs_stride;
+        for (int j = tid; j < p.V; j += WIDE_THREADS) out[j] = 0.0;
+        __syncthreads();
+        for (int i = tid; i < keep; i += WIDE_THREADS) out[wkey_id(sk[i])] = p_of(i) / F;
+        return;
+    }
     // R3: cap_per_token_bits -- entropy of the renormalised support; bisect tau on softmax(log(f+1e-12)/tau)
     // over every id (float64, libm-equivalent log/exp: tolerance-level)
     if (p.rk_cap > 0 && n > 0) {

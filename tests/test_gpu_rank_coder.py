@@ -7,6 +7,7 @@ kernel is compared with the oracle (same canonical order) and the capacities wit
 
 from __future__ import annotations
 
+import numpy as np
 import pytest
 
 from neuralsteganography_amd import synthetic
@@ -74,3 +75,34 @@ def test_rank_provider_behind_batched_front_end():
     res = stego_encode_batch(msgs, chunk_bytes=32, quality=q, lm=lm)
     lm.load_states(lm.drain_states())
     assert stego_decode_batch([list(r) for r in res], quality=q, lm=lm) == msgs
+
+
+@pytest.mark.parametrize("quality", [{}, {"top_k": 300}, {"top_p": 0.9}, {"min_prob": 1e-5},
+                                     {"top_k": 2000, "top_p": 0.95, "min_prob": 1e-7}])
+def test_next_token_probs_matches_reference_formula(quality):
+    """HipTransformersLM.next_token_probs vs codec/distribution.py:134-147 restated in numpy float64
+    (softmax of logits/T, apply_quality support, renormalised); 1e-12 absolute."""
+    from neuralsteganography_amd.codec.distribution import HipTransformersLM
+
+    V, T = 50257, 0.8
+    lm = HipTransformersLM(batched_lm=synthetic.SyntheticBatchedLM(9, V, 3.0, "f32"), temperature=T, **quality)
+    got0 = lm.next_token_probs([5, 6, 7])
+    got1 = lm.next_token_probs([5, 6, 7, 11])  # extends the context: KV step
+    for t, got in enumerate((got0, got1)):
+        x = synthetic.logits_row(9, 0, t, V, 3.0).astype(np.float64)
+        z = x / T
+        p = np.exp(z - z.max())
+        p /= p.sum()
+        order = np.lexsort((np.arange(V), -x))
+        keep = np.ones(V, bool)
+        if "top_k" in quality:
+            keep[order[quality["top_k"]:]] = False
+        if "top_p" in quality:
+            cut = np.searchsorted(np.cumsum(p[order]), quality["top_p"], side="left")
+            keep[order[cut + 1:]] = False
+        if "min_prob" in quality:
+            keep &= p >= quality["min_prob"]
+        want = np.where(keep, p, 0.0)
+        want /= want.sum()
+        assert np.abs(got - want).max() < 1e-12
+        assert (got > 0).sum() == keep.sum()
