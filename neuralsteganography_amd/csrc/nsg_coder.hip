@@ -530,6 +530,8 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + wv);
     if (b >= p.B) return;
 
+    NSG_STAMP_RT(p, b, lane, 9);
+    NSG_STAMP(p, b, lane, 0);
     ns_stream_state st = p.state[b];
     if (st.flags & NS_ST_DONE) return;
     int64_t nbits = 0;
@@ -559,6 +561,11 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     cand.ncompact = 0;
     cand.thr = -__builtin_inff();
     int nfallback = 0;
+
+    // the streaming ring's first tiles go out before the sample: they land while the threshold is computed
+    uint4 buf[PREFETCH];
+#pragma unroll
+    for (int d = 0; d < PREFETCH; ++d) buf[d] = rd.vec(d * WAVE + lane);
 
     // ---------------- prologue: stratified sample -> softmax reference r and speculative threshold -----
     // 16 blocks of 64 ids spread over the row (16 values per lane).  r = sample max (fast-sum reference);
@@ -598,14 +605,12 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     }
     if (p.flags & NS_STEP_DIAG_NO_CANDIDATES) cand.thr = __builtin_inff();
 
+    NSG_STAMP(p, b, lane, 1);
     // ---------------- streaming pass (the HBM-bound part) ----------------
     double acc64 = 0.0;
     double b64 = 0.0, u64 = 0.0;  // STATS: sum e (x-r), sum exp(x-r) untempered
     int bi = 0;
     int next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
-    uint4 buf[PREFETCH];
-#pragma unroll
-    for (int d = 0; d < PREFETCH; ++d) buf[d] = rd.vec(d * WAVE + lane);
     if (p.spec_j <= 0) {  // no sample (small vocab): reference = max of the first tile
         float x[W];
         Elem<T>::unpack(buf[0], x);
@@ -672,6 +677,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
             process(x, tile + d);
         }
     }
+    NSG_STAMP(p, b, lane, 2);
     // speculation check: the buffer holds the true top-K iff at least K elements passed the guess
     // (or a compaction happened, which needs > CAND - TS >= K passes).  Else re-stream, exactly.
     if (spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) {
@@ -697,8 +703,11 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     // ---------------- exact top-K, ranked ----------------
     uint64_t* keys = cand.keys;
+    NSG_STAMP(p, b, lane, 3);
     to_keys(cand, lane);
+    NSG_STAMP(p, b, lane, 4);
     if (cand.cnt > K) compact_topk(keys, cand.scr, cand.cnt, K, lane);
+    NSG_STAMP(p, b, lane, 5);
     const int nsk = (K + WAVE - 1) / WAVE;
     const int K8 = (K + 7) & ~7;
     if (lane < K8 - K) keys[K + lane] = 0ull;  // zero pad: never counted as greater
@@ -740,6 +749,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         return;
     }
 
+    NSG_STAMP(p, b, lane, 6);
     // ---------------- CDF step (canonical float64) ----------------
     const double m = (double)key_val(__shfl(sk[0], 0));
     double e[NSK];
@@ -939,6 +949,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         }
     }
 
+    NSG_STAMP(p, b, lane, 7);
     // state update: cross-lane values are gathered by shuffles, every lane computes the same scalars
     if (err == 0u) {
         const int P = p.P;
@@ -1003,6 +1014,8 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
             p.trace[b] = tr;
         }
     }
+    NSG_STAMP(p, b, lane, 8);
+    NSG_STAMP_RT(p, b, lane, 10);
     // rare-event diagnostics only (no per-step atomics): sharded by block so waves never contend
     const int overflow = cand.ncompact;
     lds_fence();
@@ -1166,6 +1179,7 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->stats = nullptr;
     ctx->ranked = nullptr;
     ctx->ranked_stride = 0;
+    ctx->stamps = nullptr;
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
@@ -1286,6 +1300,7 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
     p.hist = d_token_hist;
     p.hist_stride = d_token_hist ? hist_stride : 0;
     p.stats = ctx->stats;
+    p.stamps = ctx->stamps;
     if (step_flags & NS_STEP_FINISH_SENT) {
         if (!ctx->sent_end) return fail(ctx, NS_ERR_CONFIG, "NS_STEP_FINISH_SENT needs ns_set_sentence_end");
         const dim3 g((B + nsg::WPB - 1) / nsg::WPB), blk(nsg::WPB * nsg::WAVE);
@@ -1427,6 +1442,14 @@ int ns_set_rank_export(ns_ctx* ctx, int32_t* d_ranked, int stride) {
     ctx->ranked_stride = d_ranked ? stride : 0;
     return NS_OK;
 }
+
+#ifdef NSG_STAMPS
+int ns_set_stamps(ns_ctx* ctx, uint64_t* d_stamps) {  // diagnostic builds only (not in the public header)
+    if (!ctx) return NS_ERR_CONFIG;
+    ctx->stamps = d_stamps;
+    return NS_OK;
+}
+#endif
 
 int ns_set_stats(ns_ctx* ctx, double* d_stats) {
     if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");

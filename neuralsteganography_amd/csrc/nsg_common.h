@@ -191,11 +191,39 @@ struct StepParams {
     const int32_t* rk_keep;   // decode: bits to keep this step, [B]
     double* probs_out;        // ns_token_probs: filtered, renormalised p by id, [B][probs_stride]
     int64_t probs_stride;
+    uint64_t* stamps;         // NSG_STAMPS diagnostic builds: s_memtime at phase boundaries, [B][16]
     // common
     ns_stream_state* state;
     ns_step_trace* trace;
     unsigned long long* counters;
 };
+
+// In-kernel phase stamps (diagnostic builds only: -DNSG_STAMPS=1, tools/stamp_phases.py)
+#ifdef NSG_STAMPS
+__device__ __forceinline__ uint64_t nsg_memtime() {
+    uint64_t t;
+    __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ __forceinline__ uint64_t nsg_realtime() {
+    uint64_t t;
+    __asm__ volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define NSG_STAMP_RT(p, b, lane, k)                                                                   \
+    do {                                                                                              \
+        const uint64_t _t = nsg_realtime();                                                           \
+        if ((p).stamps && (lane) == 0) (p).stamps[(int64_t)(b) * 16 + (k)] = _t;                     \
+    } while (0)
+#define NSG_STAMP(p, b, lane, k)                                                                      \
+    do {                                                                                              \
+        const uint64_t _t = nsg_memtime();                                                            \
+        if ((p).stamps && (lane) == 0) (p).stamps[(int64_t)(b) * 16 + (k)] = _t;                     \
+    } while (0)
+#else
+#define NSG_STAMP(p, b, lane, k) ((void)0)
+#define NSG_STAMP_RT(p, b, lane, k) ((void)0)
+#endif
 
 // counter-based 64-bit draw, identical to or_rand64 (oracle/nsg_oracle.c): splitmix64 finaliser
 __device__ __forceinline__ uint64_t rand64(uint64_t seed, int64_t gid, int64_t t) {

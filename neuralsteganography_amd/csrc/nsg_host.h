@@ -51,6 +51,7 @@ struct ns_ctx {
     double* stats;            // encode statistics sink [B][4] (ns_set_stats), nullable
     int32_t* ranked;          // decode rank export [B][ranked_stride] (ns_set_rank_export), nullable
     int ranked_stride;
+    uint64_t* stamps;         // NSG_STAMPS diagnostic builds: per-stream phase stamps
     std::string err;
 };
 
