@@ -154,12 +154,17 @@ int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_
 
 /* Quality policies of the src rank coder (src/neuralstego/codec/quality.py:57-141 apply_quality /
  * cap_bits_per_token, keys as codec/arithmetic.py:345-362 reads them).  Off: top_k <= 0, cap_bits <= 0,
- * top_p <= 0, min_prob < 0. */
+ * top_p <= 0, min_prob < 0, prob_temp <= 0.
+ * prob_temp > 0 selects the crypto quality LM instead (src/neuralstego/crypto/arithmetic.py:20-40 +
+ * crypto/quality.py:15-89): the temperature acts on the PROBABILITIES, p' = normalise(exp(log(p + 1e-12)/T
+ * - max)), which gives every id nonzero mass, and top_k / top_p then filter p' (min_prob and cap_bits are
+ * not part of that policy and must be off).  prob_temp == 1 (math.isclose) leaves p unchanged. */
 typedef struct ns_rank_quality {
     int32_t top_k;
     int32_t cap_bits;
     double top_p;
     double min_prob;
+    double prob_temp;
 } ns_rank_quality;
 
 /* One step of the src package's own coder, the uniform rank coder of encode_with_lm

@@ -55,7 +55,7 @@ class NsRankQuality(ctypes.Structure):
     """``ns_rank_quality`` (include/nsg_coder.h)."""
 
     _fields_ = [("top_k", ctypes.c_int32), ("cap_bits", ctypes.c_int32), ("top_p", ctypes.c_double),
-                ("min_prob", ctypes.c_double)]
+                ("min_prob", ctypes.c_double), ("prob_temp", ctypes.c_double)]
 
 
 def lib() -> ctypes.CDLL:

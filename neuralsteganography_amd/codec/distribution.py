@@ -83,6 +83,7 @@ class HipTransformersLM:
         self.temperature = float(temperature)
         self.max_context = max_context
         self._q = rank_quality({"top_k": top_k, "top_p": top_p, "min_prob": min_prob})
+        self._filters = (top_k, top_p, min_prob)
         params = CoderParams(vocab=self.vocab, precision=16, temp=1.0, topk=self.vocab, dtype=logits_dtype, banned=[])
         self._ctx = CoderContext(params, max_batch=1)
         dev = torch.device("cuda", self._ctx.device)
@@ -97,6 +98,10 @@ class HipTransformersLM:
         return int(getattr(self.lm.shape, "n_positions", 0)) or None
 
     def next_token_probs(self, context_ids: Sequence[int]) -> np.ndarray:
+        return self._probs_with(context_ids, self._q)
+
+    def _probs_with(self, context_ids: Sequence[int], q) -> np.ndarray:
+        """next_token_probs under the quality struct ``q`` (the crypto quality LM passes its own)."""
         import torch
 
         from ..coder import _ptr, _stream_handle
@@ -115,7 +120,7 @@ class HipTransformersLM:
         self._last = ctx
         lg = self._logits
         rc = _lib.lib().ns_token_probs(self._ctx._h, _ptr(lg), lg.stride(0), 1, self.temperature,
-                                       ctypes.byref(self._q), _ptr(self._probs), self._probs.stride(0),
+                                       ctypes.byref(q), _ptr(self._probs), self._probs.stride(0),
                                        _ptr(self._state), _stream_handle())
         self._ctx.check(rc, "ns_token_probs")
         return self._probs[0].cpu().numpy().copy()

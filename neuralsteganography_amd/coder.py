@@ -550,6 +550,8 @@ def rank_quality(quality) -> "_lib.NsRankQuality":
             q["min_prob"] = float(value)
         elif k in ("cap_per_token_bits", "cap_bits_per_token"):
             q["cap"] = int(value)
+        elif k == "prob_temp":  # crypto quality LM (crypto/quality.py:57-64): temperature on probabilities
+            q["prob_temp"] = float(value)
     if "top_k" in q and q["top_k"] <= 0:
         raise ConfigurationError("top_k must be positive")
     if "top_p" in q and not 0 < q["top_p"] <= 1:
@@ -558,7 +560,12 @@ def rank_quality(quality) -> "_lib.NsRankQuality":
         raise ConfigurationError("min_prob must be non-negative")
     if "cap" in q and q["cap"] <= 0:
         raise ConfigurationError("cap_per_token_bits must be positive")
-    return _lib.NsRankQuality(q.get("top_k", 0), q.get("cap", 0), q.get("top_p", 0.0), q.get("min_prob", -1.0))
+    if "prob_temp" in q and q["prob_temp"] <= 0:
+        raise ConfigurationError("temperature must be positive")
+    if "prob_temp" in q and ("cap" in q or "min_prob" in q):
+        raise ConfigurationError("the crypto quality policy takes only top_k, top_p and temperature")
+    return _lib.NsRankQuality(q.get("top_k", 0), q.get("cap", 0), q.get("top_p", 0.0), q.get("min_prob", -1.0),
+                              q.get("prob_temp", 0.0))
 
 
 class RankEncodeSession:

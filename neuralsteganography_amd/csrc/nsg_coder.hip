@@ -1143,7 +1143,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.6 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.7 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -1365,6 +1365,8 @@ static int rank_prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, i
     if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
     if (!q) return fail(ctx, NS_ERR_CONFIG, "rank step: null quality");
     if (q->top_p > 1.0) return fail(ctx, NS_ERR_CONFIG, "top_p must be within (0, 1]");
+    if (q->prob_temp > 0.0 && (q->cap_bits > 0 || q->min_prob >= 0.0))
+        return fail(ctx, NS_ERR_CONFIG, "crypto quality (prob_temp) takes only top_k and top_p");
     if (ctx->vocab > 0x1FFFF) return fail(ctx, NS_ERR_UNSUPPORTED, "rank coder: vocab must be < 131072");
     if (!ctx->wide.keys_in && nsg_wide_alloc(ctx) != NS_OK) {
         nsg_wide_free(ctx);
@@ -1377,6 +1379,9 @@ static int rank_prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, i
     p.rk_cap = q->cap_bits;
     p.rk_top_p = q->top_p;
     p.rk_min_prob = q->min_prob;
+    // crypto/quality.py:60: the temperature step runs unless math.isclose(T, 1.0) (rel_tol 1e-9)
+    const double pt = q->prob_temp;
+    p.rk_ptemp = (pt > 0.0 && fabs(pt - 1.0) > 1e-9 * fmax(pt, 1.0)) ? pt : 0.0;
     return NS_OK;
 }
 

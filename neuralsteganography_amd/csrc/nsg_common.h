@@ -187,6 +187,7 @@ struct StepParams {
     int rk_top_k, rk_cap;     // <= 0: off
     double rk_top_p;          // <= 0: off
     double rk_min_prob;       // < 0: off
+    double rk_ptemp;          // crypto quality LM: temperature on the probabilities (<= 0: off)
     int32_t* rk_cons;         // encode: bits consumed per token, [B][hist_stride]
     const int32_t* rk_keep;   // decode: bits to keep this step, [B]
     double* probs_out;        // ns_token_probs: filtered, renormalised p by id, [B][probs_stride]

@@ -643,6 +643,26 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
         if (i < fz && e_of(i) == 0.0) fz = i;
     int n = block_min_int(fz, smi);
 
+    // R1c: crypto quality LM (crypto/quality.py:57-64): temperature on the probabilities,
+    // q_i = exp(log(p_i + 1e-12)/T - max) normalised -- every id keeps mass unless exp underflows.
+    // Monotone in p, so the rank order is unchanged; libm-equivalent log/exp (tolerance-level).
+    const double Tq = p.rk_ptemp;
+    const bool crypto = Tq > 0.0;
+    double a0 = 0.0, Q = 1.0;
+    if (crypto) {
+        a0 = log(p_of(0) + 1e-12) / Tq;
+        double ql = 0.0;
+        int zq = V;
+        for (int i = tid; i < V; i += WIDE_THREADS) {
+            const double q = exp(log(p_of(i) + 1e-12) / Tq - a0);
+            ql += q;
+            if (q == 0.0 && i < zq) zq = i;
+        }
+        Q = block_sum(ql, sm64);
+        n = block_min_int(zq, smi);
+    }
+    auto pf = [&](int i) -> double { return crypto ? exp(log(p_of(i) + 1e-12) / Tq - a0) / Q : p_of(i); };
+
     // R2: top_k, top_p (left-to-right cumsum, searchsorted 'left'), min_prob
     if (p.rk_top_k > 0) n = min(n, p.rk_top_k);
     if (p.rk_top_p > 0.0) {
@@ -652,7 +672,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
         }
         __syncthreads();
         for (int base = 0; base < V; base += WIDE_ROUND) {
-            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? p_of(base + i) : 0.0;
+            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? pf(base + i) : 0.0;
             __syncthreads();
             if (tid == 0 && cut_sh == V) {
                 double a = acc_sh;
@@ -673,7 +693,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
     if (p.rk_min_prob >= 0.0) {
         int fm = V;
         for (int i = tid; i < V; i += WIDE_THREADS)
-            if (i < fm && !(p_of(i) >= p.rk_min_prob)) fm = i;
+            if (i < fm && !(pf(i) >= p.rk_min_prob)) fm = i;
         n = min(n, block_min_int(fm, smi));
     }
     // next_token_probs (codec/distribution.py:107-142): the quality-filtered support renormalised, by id
@@ -681,28 +701,28 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
         const bool filtered = p.rk_top_k > 0 || p.rk_top_p > 0.0 || p.rk_min_prob >= 0.0;
         const int keep = filtered ? n : V;
         double fl = 0.0;
-        for (int i = tid; i < keep; i += WIDE_THREADS) fl += p_of(i);
+        for (int i = tid; i < keep; i += WIDE_THREADS) fl += pf(i);
         const double F = block_sum(fl, sm64);
         double* out = p.probs_out + (int64_t)b * p.probs_stride;
         for (int j = tid; j < p.V; j += WIDE_THREADS) out[j] = 0.0;
         __syncthreads();
-        for (int i = tid; i < keep; i += WIDE_THREADS) out[wkey_id(sk[i])] = p_of(i) / F;
+        for (int i = tid; i < keep; i += WIDE_THREADS) out[wkey_id(sk[i])] = pf(i) / F;
         return;
     }
     // R3: cap_per_token_bits -- entropy of the renormalised support; bisect tau on softmax(log(f+1e-12)/tau)
     // over every id (float64, libm-equivalent log/exp: tolerance-level)
     if (p.rk_cap > 0 && n > 0) {
         double fl = 0.0;
-        for (int i = tid; i < n; i += WIDE_THREADS) fl += p_of(i);
+        for (int i = tid; i < n; i += WIDE_THREADS) fl += pf(i);
         const double F = block_sum(fl, sm64);
         double hl = 0.0;
         for (int i = tid; i < n; i += WIDE_THREADS) {
-            const double f = p_of(i) / F;
+            const double f = pf(i) / F;
             if (f > 0.0) hl -= f * log2(f);
         }
         const double H = block_sum(hl, sm64);
         if (H > (double)p.rk_cap) {
-            const double lf0 = log(p_of(0) / F + 1e-12);
+            const double lf0 = log(pf(0) / F + 1e-12);
             double low = 1e-6, high = 1.0;
             int n_target = n;
             for (int it = 0; it < 60; ++it) {
@@ -711,7 +731,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
                 double sl = 0.0, tl = 0.0;
                 int zl = V;
                 for (int i = tid; i < V; i += WIDE_THREADS) {
-                    const double f = i < n ? p_of(i) / F : 0.0;
+                    const double f = i < n ? pf(i) / F : 0.0;
                     const double a = log(f + 1e-12) / mid - mx;
                     const double c = exp(a);
                     if (c > 0.0) {

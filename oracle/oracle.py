@@ -31,7 +31,7 @@ class OrState(ctypes.Structure):
 
 class OrRankQuality(ctypes.Structure):
     _fields_ = [("top_k", ctypes.c_int32), ("top_p", ctypes.c_double), ("min_prob", ctypes.c_double),
-                ("cap_bits", ctypes.c_int32)]
+                ("cap_bits", ctypes.c_int32), ("prob_temp", ctypes.c_double)]
 
 
 def rank_quality(quality) -> OrRankQuality:
@@ -39,7 +39,7 @@ def rank_quality(quality) -> OrRankQuality:
     q = dict(quality or {})
     return OrRankQuality(int(q.get("top_k") or 0), float(q.get("top_p") or 0.0),
                          float(q["min_prob"]) if q.get("min_prob") is not None else -1.0,
-                         int(q.get("cap_per_token_bits") or 0))
+                         int(q.get("cap_per_token_bits") or 0), float(q.get("prob_temp") or 0.0))
 
 
 class OrTrace(ctypes.Structure):

@@ -276,6 +276,51 @@ def run_rank_config(name, cfg):
     return out
 
 
+# crypto quality LM (src/neuralstego/crypto/arithmetic.py encode_arithmetic / decode_arithmetic over
+# _QualityControlledLM + crypto/quality.py apply_quality): name -> vocab, logit scale, crypto quality
+# (temperature on probabilities, top_k, top_p), payload bytes per stream.  Base provider: the untempered
+# _ModelAdapter softmax (RowProvider with temp 1.0).
+CRYPTO_CONFIGS = {
+    "k1_v50257_t08_k5000": dict(vocab=50257, scale=3.0, quality={"temperature": 0.8, "top_k": 5000}, nbytes=[64, 7]),
+    "k2_v50257_t13_p09": dict(vocab=50257, scale=3.0, quality={"temperature": 1.3, "top_p": 0.9}, nbytes=[60, 5]),
+    "k3_v50257_t07": dict(vocab=50257, scale=3.0, quality={"temperature": 0.7}, nbytes=[30, 2]),
+    "k4_v700_t1_k300_p095": dict(vocab=700, scale=2.0, quality={"top_k": 300, "top_p": 0.95}, nbytes=[20]),
+}
+
+
+def crypto_rank_quality(q):
+    """The crypto policy as the build's rank-kernel quality keys (prob_temp = temperature on probabilities)."""
+    out = {"prob_temp": float(q.get("temperature", 1.0))}
+    for k in ("top_k", "top_p"):
+        if q.get(k) is not None:
+            out[k] = q[k]
+    return out
+
+
+def run_crypto_config(name, cfg):
+    sys.path.insert(0, str(REF / "src"))
+    from neuralstego.crypto import arithmetic as crypto_coder  # src/neuralstego/crypto/arithmetic.py
+
+    assert Path(crypto_coder.__file__).resolve() == (REF / "src/neuralstego/crypto/arithmetic.py").resolve()
+    out = {"tokens": [], "tok_off": [0], "cons": [], "payload": [], "pay_off": [0], "decoded": [], "dec_off": [0]}
+    for s, nbytes in enumerate(cfg["nbytes"]):
+        payload = synthetic.payload_bytes(s, nbytes)
+        prov = RowProvider(LOGIT_SEED, s, cfg["vocab"], cfg["scale"], 1.0)
+        toks, state = crypto_coder.encode_arithmetic(payload, prov, quality=cfg["quality"],
+                                                     seed_text=synthetic.DEFAULT_CONTEXT)
+        dprov = RowProvider(LOGIT_SEED, s, cfg["vocab"], cfg["scale"], 1.0)
+        dec = crypto_coder.decode_arithmetic(toks, dprov, quality=cfg["quality"], seed_text=synthetic.DEFAULT_CONTEXT,
+                                             state=dict(state))
+        assert dec == payload, f"{name} stream {s}: reference round trip failed"
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["cons"] += list(state["history"])
+        out["payload"] += list(payload); out["pay_off"].append(len(out["payload"]))
+        out["decoded"] += list(dec); out["dec_off"].append(len(out["decoded"]))
+        print(f"  {name} s={s} bytes={nbytes} tokens={len(toks)} bits/token={8 * nbytes / max(1, len(toks)):.2f}",
+              flush=True)
+    return out
+
+
 def run_compat_config(name, cfg, ref, stable_sort_mode):
     from tests.golden.toy_tokenizer import ToyTokenizer
 
@@ -311,6 +356,21 @@ def run_compat_config(name, cfg, ref, stable_sort_mode):
 
 def main(names=None):
     ref, stable = _import_reference()
+    for name, cfg in CRYPTO_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_crypto_config(name, cfg)
+        meta = dict(cfg, name=name, kind="crypto", temp=1.0, crypto_quality=cfg["quality"],
+                    quality=crypto_rank_quality(cfg["quality"]), logit_seed=LOGIT_SEED,
+                    payload_seed=synthetic.PAYLOAD_SEED, context=synthetic.DEFAULT_CONTEXT,
+                    reference="src/neuralstego/crypto/arithmetic.py encode_arithmetic / decode_arithmetic")
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            consumed=np.asarray(res["cons"], dtype=np.int32),
+            payload=np.asarray(res["payload"], dtype=np.uint8), pay_off=np.asarray(res["pay_off"], np.int64),
+            decoded=np.asarray(res["decoded"], dtype=np.uint8), dec_off=np.asarray(res["dec_off"], np.int64))
     for name, cfg in RANK_CONFIGS.items():
         if names and name not in names:
             continue

@@ -106,3 +106,58 @@ def test_next_token_probs_matches_reference_formula(quality):
         want /= want.sum()
         assert np.abs(got - want).max() < 1e-12
         assert (got > 0).sum() == keep.sum()
+
+
+@pytest.mark.parametrize("name", golden.crypto_names())
+def test_crypto_quality_lm_matches_reference(name):
+    """crypto.encode_arithmetic / decode_arithmetic (crypto/arithmetic.py:43-91) on the HIP rank kernel with the
+    temperature-on-probabilities policy: tokens, history and payload equal the reference run's."""
+    from neuralsteganography_amd.crypto import decode_arithmetic, encode_arithmetic
+
+    g = golden.load_rank(name)
+    m = g.meta
+    for s in g.streams:
+        lm = _provider(g, [s.stream])
+        caller_state = {}
+        toks, st = encode_arithmetic(s.payload, lm, quality=m["crypto_quality"], seed_text=m["context"],
+                                     state=caller_state)
+        assert toks == s.tokens, f"{name} stream {s.stream}: tokens differ from the reference"
+        assert list(st["history"]) == s.consumed and caller_state["history"] == st["history"]
+        lm2 = _provider(g, [s.stream])
+        assert decode_arithmetic(toks, lm2, quality=m["crypto_quality"], seed_text=m["context"], state=st) == s.payload
+    with pytest.raises(ValueError):
+        decode_arithmetic([1, 2], _provider(g, [0]), quality=m["crypto_quality"])
+
+
+@pytest.mark.parametrize("quality", [{"temperature": 0.7}, {"temperature": 1.3, "top_k": 3000},
+                                     {"temperature": 0.9, "top_p": 0.8}, {"top_k": 100}])
+def test_crypto_quality_controlled_probs_match_reference_formula(quality):
+    """QualityControlledLM.next_token_probs vs crypto/quality.py:57-89 restated in numpy float64 over the
+    HipTransformersLM softmax; 1e-12 absolute, same support."""
+    from neuralsteganography_amd.codec.distribution import HipTransformersLM
+    from neuralsteganography_amd.crypto import QualityControlledLM
+
+    V = 50257
+    base = HipTransformersLM(batched_lm=synthetic.SyntheticBatchedLM(13, V, 3.0, "f32"))
+    lm = QualityControlledLM(base, top_k=quality.get("top_k"), top_p=quality.get("top_p"),
+                             temperature=quality.get("temperature", 1.0))
+    got = lm.next_token_probs([5, 6, 7])
+    x = synthetic.logits_row(13, 0, 0, V, 3.0).astype(np.float64)
+    p = np.exp(x - x.max())
+    p /= p.sum()
+    T = quality.get("temperature", 1.0)
+    if T != 1.0:
+        a = np.log(p + 1e-12) / T
+        p = np.exp(a - a.max())
+        p /= p.sum()
+    order = np.lexsort((np.arange(V), -x))
+    keep = np.ones(V, bool)
+    if "top_k" in quality:
+        keep[order[quality["top_k"]:]] = False
+    if "top_p" in quality:
+        cut = np.searchsorted(np.cumsum(p[order]), quality["top_p"], side="left")
+        keep[order[cut + 1:]] = False
+    want = np.where(keep, p, 0.0)
+    want /= want.sum()
+    assert np.abs(got - want).max() < 1e-12
+    assert (got > 0).sum() == keep.sum()

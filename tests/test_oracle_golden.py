@@ -149,3 +149,33 @@ def test_oracle_rank_coder_matches_reference(name):
             assert toks == s.tokens
         dec = oracle.rank_decode_stream(row, toks, cons, 8 * len(s.payload), temp=m["temp"], quality=m["quality"])
         assert dec == s.payload == s.decoded
+
+
+@pytest.mark.parametrize("name", golden.crypto_names())
+def test_oracle_crypto_quality_matches_reference(name):
+    """The crypto quality LM (crypto/arithmetic.py:20-123 + crypto/quality.py:15-89: temperature on the
+    probabilities, then top_k / top_p) in front of the rank coder: tokens, consumption and the round trip equal
+    the reference run's (canonical step R1c of oracle/nsg_oracle.c)."""
+    g = golden.load_rank(name)
+    m = g.meta
+    assert m["kind"] == "crypto" and "prob_temp" in m["quality"]
+    for s in g.streams:
+        row = lambda t, s=s: g.row(s.stream, t)
+        toks, cons = oracle.rank_encode_stream(row, s.payload, temp=m["temp"], quality=m["quality"])
+        assert cons == s.consumed and toks == s.tokens
+        dec = oracle.rank_decode_stream(row, toks, cons, 8 * len(s.payload), temp=m["temp"], quality=m["quality"])
+        assert dec == s.payload == s.decoded
+
+
+def test_crypto_quality_extraction_and_validation():
+    """crypto/arithmetic.py:94-117 _extract_quality and crypto/quality.py's QualityConfigError domains."""
+    from neuralsteganography_amd.codec.errors import QualityConfigError
+    from neuralsteganography_amd.crypto.arithmetic import _extract_quality, _rank_quality
+
+    assert _extract_quality(None) == {"top_k": None, "top_p": None, "temperature": 1.0}
+    assert _extract_quality({"top_k": "7", "temperature": 2}) == {"top_k": 7, "top_p": None, "temperature": 2.0}
+    assert _rank_quality(None, None, 1.0 + 1e-12) == {"prob_temp": 1.0}  # math.isclose: no tempering
+    assert _rank_quality(5, 0.5, 0.7) == {"prob_temp": 0.7, "top_k": 5, "top_p": 0.5}
+    for bad in [(None, None, 0.0), (0, None, 1.0), (None, 1.5, 1.0), (None, 0.0, 1.0)]:
+        with pytest.raises(QualityConfigError):
+            _rank_quality(*bad)
