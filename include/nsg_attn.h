@@ -1,0 +1,38 @@
+/*
+ * nsg_attn.h -- decode-step attention of the batched GPT-2 forward (row a19 of SURVEY.md §8), part of
+ * `libnsgcoder.so`.
+ *
+ * Replaces, for one new token per stream, the attention of the reference's per-token forward
+ * `model(prev, past_key_values=past, position_ids=...)` (code_base/arithmetic.py:115-122, the Hugging Face
+ * GPT2Attention over the whole unbounded cache: softmax(q k^T / sqrt(D)) v).  It fuses the KV append of
+ * the new token with the attention over the cache: one wavefront per (stream, head) streams the K and V rows
+ * of that head once from HBM (online softmax in fp32), so the step is HBM-bound at B*(L+1)*2*D*2 bytes per
+ * layer.  fp16 in and out, fp32 accumulation; no allocation, stream-ordered on the caller's hipStream_t.
+ */
+#ifndef NSG_ATTN_H
+#define NSG_ATTN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One layer, one decode position.
+ *   d_qkv     fp16 [B, qkv_stride]: q at columns [0, H*D), k at [H*D, 2*H*D), v at [2*H*D, 3*H*D) (the c_attn
+ *             output of GPT-2, head h at columns h*D..h*D+D-1 of each part).
+ *   d_k_cache, d_v_cache  fp16, element (b, h, j, d) at b*cache_b_stride + h*cache_h_stride + j*D + d.
+ *   L0        positions already cached; the call writes the new k/v at position L0 and attends to
+ *             positions 0..L0 (L0 + 1 keys).  The caller guarantees L0 < the cache's capacity.
+ *   d_out     fp16 [B, out_stride]: head h of stream b at columns h*D..h*D+D-1.
+ *   scale     the score scale (1/sqrt(D) for GPT-2).
+ * D must be 64.  Returns 0, or a negative NS_ERR_* code of nsg_coder.h on bad arguments / launch failure. */
+int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                        int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0, void* d_out,
+                        int64_t out_stride, float scale, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NSG_ATTN_H */

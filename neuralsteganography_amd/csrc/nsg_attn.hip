@@ -1,0 +1,158 @@
+// Decode-step attention of the batched GPT-2 forward with the KV append fused in (include/nsg_attn.h).
+//
+// Reference semantics: Hugging Face GPT2Attention for one new token per stream over the unbounded cache the
+// reference keeps (code_base/arithmetic.py:115-122): softmax(q k^T / sqrt(D)) v over positions 0..L0.
+//
+// Layout: one wavefront per (stream, head).  Lane l holds dims 8*(l&7)..+7 of key row (l>>3) of an 8-row
+// chunk, so an 8-lane group reads one 128-byte K (and V) row and the wave reads 1 KiB of contiguous cache per
+// 16-byte load instruction.  Scores are reduced inside the 8-lane group; each group keeps its own online
+// softmax (running max, sum, 8 accumulator dims) over the rows it saw, and the 8 groups are merged once at the
+// end.  fp16 q.k products with fp32 accumulation (v_dot2_f32_f16), exp2 with log2(e) folded into the scale.
+// HBM-bound: 2*(L0+1)*128 bytes per (stream, head) read once, non-temporal (the rows are not reused within
+// the step).  The new token's k/v come from the qkv registers and are written to the cache by group 0.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nsg_attn.h"
+#include "nsg_coder.h"
+
+namespace nsg {
+
+constexpr int ATT_D = 64;
+constexpr int ATT_WAVES = 4;  // (stream, head) pairs per 256-thread workgroup
+constexpr int ATT_U = 4;      // 8-row chunks per loop iteration: 32 keys per wave in flight
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float dot8(f16x8 a, f16x8 b) {
+    float s = 0.0f;
+    s = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 0, 1), __builtin_shufflevector(b, b, 0, 1), s, false);
+    s = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 2, 3), __builtin_shufflevector(b, b, 2, 3), s, false);
+    s = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 4, 5), __builtin_shufflevector(b, b, 4, 5), s, false);
+    s = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 6, 7), __builtin_shufflevector(b, b, 6, 7), s, false);
+    return s;
+}
+
+__device__ __forceinline__ void unpack8(f16x8 v, float* f) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+
+__global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Float16* __restrict__ qkv,
+                                                                     int64_t qkv_stride, _Float16* kc, _Float16* vc,
+                                                                     int64_t cb, int64_t ch, int B, int H, int L0,
+                                                                     _Float16* __restrict__ out, int64_t out_stride,
+                                                                     float scale_log2) {
+    const int lane = threadIdx.x & 63;
+    const int pair = blockIdx.x * ATT_WAVES + (threadIdx.x >> 6);
+    if (pair >= B * H) return;
+    const int b = pair / H;
+    const int h = pair - b * H;
+    const int g = lane >> 3;  // row within an 8-row chunk
+    const int c = lane & 7;   // 8-dim slice
+    const int C = H * ATT_D;
+    const _Float16* qrow = qkv + (int64_t)b * qkv_stride + h * ATT_D + c * 8;
+    const f16x8 q = *(const f16x8*)qrow;
+    const f16x8 knew = *(const f16x8*)(qrow + C);
+    const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
+    _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
+    _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
+    if (g == 0) {  // KV append of the new token (position L0)
+        *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
+        *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
+    }
+    const int Lk = L0 + 1;
+    const int last_cached = L0 > 0 ? L0 - 1 : 0;
+    float m = -1e30f, l = 0.0f;
+    float acc[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+
+    for (int j0 = 0; j0 < Lk; j0 += 8 * ATT_U) {
+        f16x8 kr[ATT_U], vr[ATT_U];
+#pragma unroll
+        for (int u = 0; u < ATT_U; ++u) {
+            const int row = min(j0 + 8 * u + g, last_cached);
+            kr[u] = __builtin_nontemporal_load((const f16x8*)(kb + (int64_t)row * ATT_D));
+            vr[u] = __builtin_nontemporal_load((const f16x8*)(vb + (int64_t)row * ATT_D));
+        }
+        float s[ATT_U];
+        bool valid[ATT_U];
+        float mx = m;
+#pragma unroll
+        for (int u = 0; u < ATT_U; ++u) {
+            const int row = j0 + 8 * u + g;
+            valid[u] = row < Lk;
+            if (row == L0) {  // the new token: from registers, not from the cache just written
+                kr[u] = knew;
+                vr[u] = vnew;
+            }
+            float sv = dot8(q, kr[u]);
+            sv += __shfl_xor(sv, 1);
+            sv += __shfl_xor(sv, 2);
+            sv += __shfl_xor(sv, 4);
+            s[u] = sv * scale_log2;
+            if (valid[u]) mx = fmaxf(mx, s[u]);
+        }
+        const float alpha = exp2f(m - mx);
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[d] *= alpha;
+#pragma unroll
+        for (int u = 0; u < ATT_U; ++u) {
+            const float p = valid[u] ? exp2f(s[u] - mx) : 0.0f;
+            l += p;
+            float v[8];
+            unpack8(vr[u], v);
+#pragma unroll
+            for (int d = 0; d < 8; ++d) acc[d] = fmaf(p, v[d], acc[d]);
+        }
+        m = mx;
+    }
+    // merge the 8 row groups (lanes c, c+8, ..., c+56 hold the same dims)
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) {
+        const float mo = __shfl_xor(m, off);
+        const float lo = __shfl_xor(l, off);
+        const float mn = fmaxf(m, mo);
+        const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
+        l = l * fa + lo * fo;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            const float ao = __shfl_xor(acc[d], off);
+            acc[d] = acc[d] * fa + ao * fo;
+        }
+        m = mn;
+    }
+    if (g == 0) {
+        const float inv = 1.0f / l;
+        f16x8 w;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = (_Float16)(acc[i] * inv);
+        *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * 8) = w;
+    }
+}
+
+}  // namespace nsg
+
+extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                                   int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
+                                   void* d_out, int64_t out_stride, float scale, void* hip_stream) {
+    if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0) return NS_ERR_CONFIG;
+    if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
+    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_k_cache | (uintptr_t)d_v_cache | (uintptr_t)d_out;
+    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || (cache_b_stride & 7) || (cache_h_stride & 7))
+        return NS_ERR_CONFIG;  // 16-byte rows
+    if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
+    if (cache_h_stride < (int64_t)(L0 + 1) * D || cache_b_stride < (int64_t)H * cache_h_stride) return NS_ERR_CONFIG;
+    if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
+    const int pairs = B * H;
+    const float scale_log2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(nsg::decode_attn_kernel, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
+                       dim3(64 * nsg::ATT_WAVES), 0, (hipStream_t)hip_stream, (const _Float16*)d_qkv, qkv_stride,
+                       (_Float16*)d_k_cache, (_Float16*)d_v_cache, cache_b_stride, cache_h_stride, B, H, L0,
+                       (_Float16*)d_out, out_stride, scale_log2);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}

@@ -9,6 +9,12 @@ forward semantics (``code_base/arithmetic.py:12-48,115-122``):
   (``_position_ids_for_cache``, ``:44-48``) and attends to the whole cache: the reference never truncates
   it (``limit_past`` slices head_dim, a no-op, ``code_base/utils.py:19-30``).
 
+Decode steps on the GPU in fp16 (the product configuration) run attention in the hand-written HIP kernel
+``ns_decode_attention`` (``csrc/nsg_attn.hip``: KV append fused with a one-pass online-softmax attention,
+one wavefront per (stream, head), HBM-bound on the cache); fp32 compute and the CPU keep PyTorch's
+``scaled_dot_product_attention`` as the forward's reference configuration (tests pin the two against each
+other and against Hugging Face).
+
 Logits are produced as ``h @ wte^T`` into a ``[B, ld]`` buffer with ``ld = row_stride(V)`` (zero weight
 columns beyond V), so the coder reads 16-byte-aligned rows without a copy.  Weights are taken from a
 Hugging Face ``GPT2LMHeadModel`` (pretrained when available offline, random-init otherwise).
@@ -81,6 +87,14 @@ class BatchedGPT2:
         self.B = 0
         self.L = 0
         self.k_cache = self.v_cache = None
+        # decode-step attention: the HIP kernel for fp16 on the GPU (fails loudly if the library is missing)
+        self.hip_attention = self.device.type == "cuda" and self.dtype == torch.float16
+        if self.hip_attention:
+            from .. import _lib
+
+            self._attn = _lib.lib().ns_decode_attention
+            if self.shape.n_embd // self.shape.n_head != 64:
+                raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
 
     # ------------------------------------------------------------------
     def allocate(self, B: int, max_len: int) -> None:
@@ -113,6 +127,8 @@ class BatchedGPT2:
         B, T, C = h.shape
         H, D = s.n_head, C // s.n_head
         a = self._ln(h, lw["ln1_w"], lw["ln1_b"])
+        if T == 1 and self.hip_attention and not causal:
+            return self._block_decode_hip(i, h, a)
         qkv = torch.addmm(lw["qkv_b"], a.reshape(B * T, C), lw["qkv_w"]).view(B, T, 3, H, D)
         q = qkv[:, :, 0].transpose(1, 2)
         k = qkv[:, :, 1].transpose(1, 2)
@@ -132,6 +148,28 @@ class BatchedGPT2:
         f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B * T, C), lw["fc_w"]), approximate="tanh")
         h = h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, T, C)
         return h
+
+    def _block_decode_hip(self, i, h, a):
+        """One decode block with the fused KV-append + attention HIP kernel (``include/nsg_attn.h``)."""
+        from ..coder import _stream_handle
+
+        s = self.shape
+        lw = self.layers[i]
+        B, _, C = h.shape
+        H, D = s.n_head, C // s.n_head
+        qkv = torch.addmm(lw["qkv_b"], a.reshape(B, C), lw["qkv_w"])  # [B, 3C] contiguous
+        o = torch.empty((B, C), device=h.device, dtype=self.dtype)
+        kc, vc = self.k_cache[i], self.v_cache[i]  # [Bmax, H, max_len, D]
+        if self.L >= kc.shape[2]:
+            raise RuntimeError("KV cache full")  # step() grows the cache before this point
+        rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+                        B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), _stream_handle())
+        if rc != 0:
+            raise RuntimeError(f"ns_decode_attention failed ({rc})")
+        h = h + torch.addmm(lw["o_b"], o, lw["o_w"]).view(B, 1, C)
+        m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
+        f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B, C), lw["fc_w"]), approximate="tanh")
+        return h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, 1, C)
 
     def _logits(self, h_last):
         hf = self._ln(h_last, self.lnf_w, self.lnf_b)

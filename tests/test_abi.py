@@ -1,4 +1,4 @@
-"""CPU: the C-ABI library loads and exports every entry point include/nsg_coder.h declares."""
+"""CPU: the C-ABI library loads and exports every entry point include/*.h declares."""
 
 import ctypes
 import re
@@ -8,11 +8,11 @@ import pytest
 
 from neuralsteganography_amd import _lib
 
-HEADER = Path(__file__).resolve().parents[1] / "include" / "nsg_coder.h"
+HEADERS = sorted((Path(__file__).resolve().parents[1] / "include").glob("*.h"))
 
 
 def declared_symbols():
-    text = HEADER.read_text()
+    text = "\n".join(h.read_text() for h in HEADERS)
     return sorted(set(re.findall(r"\b(ns_[a-z_0-9]+)\s*\(", text)))
 
 

@@ -179,3 +179,71 @@ def test_batched_front_end_multi_message_roundtrip():
     assert [r.metadata.total for r in res] == [1, 1, 3, 1]
     lm.load_states([])  # decode must not depend on the bit-count side channel
     assert stego_decode_batch([list(r) for r in res], quality=q, seed_text="seed", lm=lm) == msgs
+
+
+@pytest.mark.parametrize("B,H,L0", [(3, 12, 0), (3, 12, 1), (5, 12, 7), (4, 16, 8), (2, 12, 33), (7, 12, 200),
+                                    (2, 16, 1023)])
+def test_hip_decode_attention_matches_fp32_reference(B, H, L0):
+    """ns_decode_attention (csrc/nsg_attn.hip) vs softmax(q k^T / sqrt(D)) v in fp32 (torch) over the cache
+    plus the appended token; the kernel must also have written the new k/v at position L0.  fp16 output:
+    2e-3 absolute on O(1) values."""
+    from neuralsteganography_amd import _lib
+    from neuralsteganography_amd.coder import _stream_handle
+
+    D, cap = 64, L0 + 5
+    g = torch.Generator(device="cuda").manual_seed(100 + L0)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kc = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    vc = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    kc0, vc0 = kc.clone(), vc.clone()
+    out = torch.full((B, H * D), float("nan"), device="cuda").half()
+    rc = _lib.lib().ns_decode_attention(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                                        kc.stride(1), B, H, D, L0, out.data_ptr(), out.stride(0), D ** -0.5,
+                                        _stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    q, k, v = qkv.view(B, 3, H, D).float().unbind(1)
+    kk = kc0.float().clone()
+    vv = vc0.float().clone()
+    kk[:, :, L0] = k
+    vv[:, :, L0] = v
+    s = torch.einsum("bhd,bhjd->bhj", q, kk[:, :, : L0 + 1]) * D ** -0.5
+    want = torch.einsum("bhj,bhjd->bhd", torch.softmax(s, -1), vv[:, :, : L0 + 1]).reshape(B, H * D)
+    assert (out.float() - want).abs().max().item() < 2e-3
+    assert torch.equal(kc[:, :, L0], k.half()) and torch.equal(vc[:, :, L0], v.half())
+    assert torch.equal(kc[:, :, :L0], kc0[:, :, :L0]) and torch.equal(kc[:, :, L0 + 1:], kc0[:, :, L0 + 1:])
+
+
+def test_hip_decode_attention_rejects_bad_shapes():
+    from neuralsteganography_amd import _lib
+
+    t = torch.zeros((2, 3 * 64), device="cuda").half()
+    c = torch.zeros((2, 1, 4, 64), device="cuda").half()
+    f = _lib.lib().ns_decode_attention
+    assert f(t.data_ptr(), t.stride(0), c.data_ptr(), c.data_ptr(), c.stride(0), c.stride(1), 2, 1, 32, 0,
+             t.data_ptr(), 64, 0.1, None) == _lib.NS_ERR_UNSUPPORTED  # head_dim 32
+    assert f(t.data_ptr(), t.stride(0), c.data_ptr(), c.data_ptr(), c.stride(0), c.stride(1), 2, 1, 64, 4,
+             t.data_ptr(), 64, 0.1, None) == _lib.NS_ERR_CONFIG  # L0 beyond the cache capacity
+
+
+def test_gpt2_fp16_decode_hip_attention_matches_sdpa_and_hf():
+    """GPT-2-small fp16 decode steps: HIP attention path vs the SDPA path on identical weights (fp16 round-off
+    only), and the last step vs Hugging Face fp32 on CPU over the whole sequence (3e-2 absolute)."""
+    from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+
+    m = random_gpt2("gpt2", seed=5)
+    a = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16)
+    b = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16)
+    b.hip_attention = False
+    assert a.hip_attention
+    ctx = synthetic.DEFAULT_CONTEXT
+    la, lb = a.prefill(ctx, 3, 4), b.prefill(ctx, 3, 4)
+    toks = [[11, 500, 9000], [7, 7, 7], [42, 43, 44], [50000, 1, 2], [3, 4, 5], [9, 8, 7]]
+    for t in toks:  # 6 steps: past the initial 4-position budget, so the cache grows once
+        tt = torch.tensor(t, device="cuda")
+        la, lb = a.step(tt), b.step(tt)
+        assert (la.float() - lb.float()).abs().max().item() < 2e-2
+    seq = list(ctx) + [t[1] for t in toks]
+    with torch.no_grad():
+        ref = m(torch.tensor([seq])).logits[0, -1]
+    assert (la[1, :50257].float().cpu() - ref).abs().max().item() < 3e-2

@@ -67,7 +67,11 @@ def main():
             lm.L = L
             return lm.step(tok)
 
+        lm.hip_attention = True
         ms_fwd, logits = timed(fwd, args.reps)
+        lm.hip_attention = False
+        ms_fwd_sdpa, _ = timed(fwd, args.reps)
+        lm.hip_attention = True
         q = torch.randn((B, H, 1, D), device=dev, dtype=lm.dtype)
 
         def attn():
@@ -77,11 +81,27 @@ def main():
                 o = F.scaled_dot_product_attention(q, kk, vv)
             return o
 
+        qkv = torch.randn((B, 3 * s.n_embd), device=dev, dtype=lm.dtype)
+        out = torch.empty((B, s.n_embd), device=dev, dtype=lm.dtype)
+        from neuralsteganography_amd import _lib
+        from neuralsteganography_amd.coder import _stream_handle
+
+        def attn_hip():
+            for i in range(s.n_layer):
+                kc, vc = lm.k_cache[i], lm.v_cache[i]
+                rc = _lib.lib().ns_decode_attention(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(),
+                                                    kc.stride(0), kc.stride(1), B, H, D, L, out.data_ptr(),
+                                                    out.stride(0), D ** -0.5, _stream_handle())
+                assert rc == 0
+            return out
+
         ms_attn, _ = timed(attn, args.reps)
+        ms_attn_hip, _ = timed(attn_hip, args.reps)
         ms_coder, _ = timed(lambda: sess.step(logits), args.reps)
         kv = B * (L + 1) * 2 * s.n_layer * s.n_embd * 2
-        print(json.dumps({"L": L, "ms_forward": ms_fwd, "ms_attention": ms_attn, "ms_coder": ms_coder,
-                          "kv_bytes": kv, "attn_GBs": kv / (ms_attn / 1e3) / 1e9,
+        print(json.dumps({"L": L, "ms_forward": ms_fwd, "ms_forward_sdpa": ms_fwd_sdpa, "ms_attention_sdpa": ms_attn,
+                          "ms_attention_hip": ms_attn_hip, "ms_coder": ms_coder, "kv_bytes": kv,
+                          "attn_sdpa_GBs": kv / (ms_attn / 1e3) / 1e9, "attn_hip_GBs": kv / (ms_attn_hip / 1e3) / 1e9,
                           "tok_per_s": B / ((ms_fwd + ms_coder) / 1e3)}), flush=True)
 
 
