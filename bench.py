@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--pool", type=int, default=6, help="distinct logit batches cycled over the steps")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
+    ap.add_argument("--e2e-batch", type=int, default=4096)
+    ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium"])
+    ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch measured by a rocprofv3 --pmc pass (corrected), if known")
     return ap.parse_args()
@@ -85,6 +89,53 @@ def cpu_baseline(pool_h, payload, nbits, args, seconds):
             "cover_tokens_per_s": steps * Bs / dt,
             "sample": f"oracle/nsg_oracle.c or_encode_batch, {Bs} streams x {steps} steps of the same logit pool "
                       f"({dt:.1f} s on 1 core)"}
+
+
+def end_to_end(args, rank, world, dev):
+    """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
+    compute, HIP decode attention) + HIP coder step per token, every stream encoding its full payload from
+    the shared 32-token context until the last stream is done (lockstep, like the reference's per-message
+    loop run for all messages at once).  Wall clock around HipArithmeticLM.encode_batch, max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.dist import reduce_job, shard_range
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    B = args.e2e_batch
+    lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.dtype,
+                         max_batch=B)
+    quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
+    context = synthetic.DEFAULT_CONTEXT
+    # warm-up: GEMM heuristics, kernels and the coder context at the same batch, short payloads
+    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality)
+    mine = shard_range(B * world, world, rank)
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.e2e_payload_bytes)) for s in mine]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    toks = lm.encode_batch(bits, context, quality=quality)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    nbits = sum(len(b) for b in bits)
+    ntok = sum(len(t) for t in toks)
+    steps = max(len(t) for t in toks)
+    bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
+    out = {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
+           "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max,
+           "lockstep_steps": steps, "ms_per_step": 1e3 * el_max / steps, "bits_per_token": bits_all / tok_all,
+           "kv_positions": lm.lm.max_len,
+           "workload": f"{args.e2e_model} (random-init weights, fp16 compute, {args.dtype} logits, HIP decode "
+                       f"attention) + ns_encode_step, {B} streams/GPU x {args.e2e_payload_bytes}-byte payloads "
+                       f"encoded to completion from a 32-token context, unbounded KV cache"}
+    del lm
+    torch.cuda.empty_cache()
+    return out
 
 
 def measured_traffic(args, version):
@@ -214,15 +265,20 @@ def main():
                      "traffic_source": traffic[1] if traffic else None,
                      "kernel": "coder_step_kernel<float,false>", "alg_bytes_per_launch": alg_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    Bs = 16
+    pool_h = [p[:Bs].float().cpu().numpy() for p in pool[:2]] if want_cpu else None
+    del pool, sess, ctx
+    torch.cuda.empty_cache()
+    if not args.no_e2e:
+        out["end_to_end"] = end_to_end(args, rank, world, dev)
+    if want_cpu:
         nb = np.asarray([len(b) for b in payload_bits], dtype=np.int64)
         stride = int((nb.max() + 7) // 8)
         pl = np.zeros((B, stride), np.uint8)
         for i, b in enumerate(payload_bits[:64]):
             pk = np.packbits(np.asarray(b, np.uint8), bitorder="little")
             pl[i, : pk.size] = pk
-        Bs = 16
-        pool_h = [p[:Bs].float().cpu().numpy() for p in pool[:2]]
         out["cpu_baseline"] = cpu_baseline(pool_h, pl, nb, args, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -97,8 +97,24 @@ class BatchedGPT2:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
 
     # ------------------------------------------------------------------
+    def kv_bytes_per_position(self, B: int) -> int:
+        s = self.shape
+        return 2 * s.n_layer * B * s.n_embd * torch.tensor([], dtype=self.dtype).element_size()
+
+    def fit_positions(self, B: int, want: int, reserve: float = 0.15) -> int:
+        """Largest cache length <= ``want`` that fits the device's free memory (keeping ``reserve`` of it for
+        activations and logits).  The reference's cache is unbounded; at B = 4096 a 1 KiB payload needs ~1.1k
+        positions (170 GB for GPT-2-small fp16), so the budget is sized from what is free, not guessed."""
+        if self.device.type != "cuda":
+            return int(want)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        if self.k_cache is not None:
+            free += 2 * self.k_cache.numel() * self.k_cache.element_size()
+        return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
+
     def allocate(self, B: int, max_len: int) -> None:
         s = self.shape
+        self.k_cache = self.v_cache = None
         hd = s.n_embd // s.n_head
         shp = (s.n_layer, B, s.n_head, max_len, hd)
         self.k_cache = torch.zeros(shp, device=self.device, dtype=self.dtype)
@@ -110,6 +126,11 @@ class BatchedGPT2:
         need more tokens than the initial budget."""
         s = self.shape
         new_len = self.max_len + int(extra)
+        if self.device.type == "cuda":  # the copy holds old and new caches at once
+            free, _ = torch.cuda.mem_get_info(self.device)
+            new_len = min(new_len, self.max_len + int(free * 0.9) // (2 * self.kv_bytes_per_position(self.B)))
+            if new_len <= self.L:
+                raise RuntimeError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
         hd = s.n_embd // s.n_head
         shp = (s.n_layer, self.B, s.n_head, new_len, hd)
         k = torch.zeros(shp, device=self.device, dtype=self.dtype)
@@ -186,7 +207,9 @@ class BatchedGPT2:
             raise ValueError("context must contain at least one token")
         if min(ctx) < 0 or max(ctx) >= self.shape.vocab:  # host check: never gather out of the table
             raise ValueError(f"context token ids must lie in [0, {self.shape.vocab})")
-        self.allocate(B, T + max_new)
+        self.allocate(B, self.fit_positions(B, T + max_new))
+        if self.max_len < T + 1:
+            raise RuntimeError(f"no device memory for a {T + 1}-position KV cache at B={B}")
         ids = torch.tensor([ctx], device=self.device, dtype=torch.long)
         pos = torch.arange(T, device=self.device) % self.shape.n_positions
         h = self.wte[ids] + self.wpe[pos][None]
