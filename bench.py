@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
+    ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
+                    help="logits handed to the coder; the fp16 head GEMM's output either way (f32 = upcast copy)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch measured by a rocprofv3 --pmc pass (corrected), if known")
     return ap.parse_args()
@@ -105,7 +107,7 @@ def end_to_end(args, rank, world, dev):
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
     B = args.e2e_batch
-    lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.dtype,
+    lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
                          max_batch=B)
     quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
     context = synthetic.DEFAULT_CONTEXT
@@ -130,7 +132,7 @@ def end_to_end(args, rank, world, dev):
            "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max,
            "lockstep_steps": steps, "ms_per_step": 1e3 * el_max / steps, "bits_per_token": bits_all / tok_all,
            "kv_positions": lm.lm.max_len,
-           "workload": f"{args.e2e_model} (random-init weights, fp16 compute, {args.dtype} logits, HIP decode "
+           "workload": f"{args.e2e_model} (random-init weights, fp16 compute, {args.e2e_logits} logits, HIP decode "
                        f"attention) + ns_encode_step, {B} streams/GPU x {args.e2e_payload_bytes}-byte payloads "
                        f"encoded to completion from a 32-token context, unbounded KV cache"}
     del lm

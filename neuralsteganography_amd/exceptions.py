@@ -36,5 +36,21 @@ class MissingChunksError(FramingError):
         return "Missing chunks at indices: " + ", ".join(str(i) for i in self.missing_indices)
 
 
+class QualityGateError(NeuralStegoError):
+    """Every cover-generation attempt was rejected by the quality gate (``exceptions.py:38-50``): the last
+    attempt's ``cover_text``, its rejection ``reasons`` and ``metrics``."""
+
+    def __init__(self, cover_text: str, reasons, metrics):
+        self.cover_text = str(cover_text)
+        self.reasons = list(reasons)
+        self.metrics = dict(metrics)
+        super().__init__(self.cover_text, self.reasons, self.metrics)
+
+    def __str__(self) -> str:
+        if not self.reasons:
+            return "quality gate rejected the generated cover"
+        return "quality gate rejected the generated cover: " + "; ".join(self.reasons)
+
+
 __all__ = ["NeuralStegoError", "ConfigurationError", "FramingError", "PacketECCError", "PacketCRCError",
-           "MissingChunksError"]
+           "MissingChunksError", "QualityGateError"]

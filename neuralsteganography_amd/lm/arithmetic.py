@@ -39,7 +39,13 @@ def coder_params_from_quality(quality: Optional[Mapping[str, object]], vocab: in
 
     temp = float(pick("temp", "temperature", default=1.0))
     precision = int(pick("precision", default=16))
-    topk = int(pick("topk", "top_k", "top-k", default=50000))
+    # top-k aliases: the LAST one in the mapping wins, as the reference's key loop does
+    # (src/neuralstego/lm/arithmetic.py:77-95) -- api.stego_encode merges {**_DEFAULT_QUALITY, **user}, so a
+    # caller's (or a regeneration attempt's) "top_k" follows the default "topk" and must override it
+    topk = 50000
+    for key, value in q.items():
+        if value is not None and key.replace("-", "_").lower() in ("topk", "top_k"):
+            topk = int(value)
     if temp <= 0:
         raise ConfigurationError("temperature must be positive")
     return CoderParams(vocab=vocab, precision=precision, temp=temp, topk=topk, dtype=logits_dtype, banned=banned)
@@ -274,6 +280,50 @@ class HipArithmeticLM:
             if t + 1 < sess.T:
                 logits = self.lm.step(sess.tok[t])
         return sess.bits()
+
+    def decode_counted(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                       quality: Mapping[str, object], done=None, check_every: int = 64):
+        """``decode_batch`` that also records, per stream, the cumulative number of bits emitted after each
+        token (the span splitter of ``text_to_spans`` needs the token at which a packet completes).  A stream
+        whose token falls outside the kept top-k stops emitting (its later counts stay flat) instead of
+        raising.  ``done(bits_lists, counts_lists) -> bool`` is polled every ``check_every`` tokens and ends
+        the loop early once it holds.  Returns ``(bits per stream, counts per stream)``."""
+        import numpy as np
+        import torch
+
+        from ..coder import _state_fields
+
+        B = len(token_lists)
+        if B == 0:
+            return [], []
+        for tl in token_lists:
+            if any((int(t) < 0 or int(t) >= self.vocab) for t in tl):
+                from ..codec.errors import DecodeDivergenceError
+
+                raise DecodeDivergenceError(f"received token id outside [0, {self.vocab})")
+        params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
+        ctx = self._coder(params, B)
+        sess = DecodeSession(ctx, token_lists)
+        counts = torch.zeros((max(sess.T, 1), B), dtype=torch.int64, device=sess.state.device)
+        logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)
+
+        def snapshot(n):
+            f = _state_fields(sess.state)
+            ob = sess.out_bits.cpu().numpy()
+            cn = counts[:n].cpu().numpy()
+            bits = [np.unpackbits(ob[i], bitorder="little")[: int(f["bit_pos"][i])].tolist() for i in range(B)]
+            return bits, [cn[: min(n, len(token_lists[i])), i].tolist() for i in range(B)]
+
+        t = 0
+        while t < sess.T:
+            sess.step(logits)
+            counts[t].copy_(sess.state[:, 2])  # bit_pos after token t
+            t += 1
+            if t < sess.T:
+                logits = self.lm.step(sess.tok[t - 1])
+            if done is not None and t % check_every == 0 and t < sess.T and done(*snapshot(t)):
+                break
+        return snapshot(t)
 
 
     def decode_tokens_repair(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,

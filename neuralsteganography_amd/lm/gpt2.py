@@ -117,8 +117,9 @@ class BatchedGPT2:
         self.k_cache = self.v_cache = None
         hd = s.n_embd // s.n_head
         shp = (s.n_layer, B, s.n_head, max_len, hd)
-        self.k_cache = torch.zeros(shp, device=self.device, dtype=self.dtype)
-        self.v_cache = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        # uninitialised: attention only ever reads positions < L + 1, all written before they are read
+        self.k_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
+        self.v_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
         self.B, self.L, self.max_len = B, 0, max_len
 
     def grow(self, extra: int) -> None:
@@ -133,8 +134,8 @@ class BatchedGPT2:
                 raise RuntimeError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
         hd = s.n_embd // s.n_head
         shp = (s.n_layer, self.B, s.n_head, new_len, hd)
-        k = torch.zeros(shp, device=self.device, dtype=self.dtype)
-        v = torch.zeros(shp, device=self.device, dtype=self.dtype)
+        k = torch.empty(shp, device=self.device, dtype=self.dtype)
+        v = torch.empty(shp, device=self.device, dtype=self.dtype)
         k[:, :, :, : self.L] = self.k_cache[:, :, :, : self.L]
         v[:, :, :, : self.L] = self.v_cache[:, :, :, : self.L]
         self.k_cache, self.v_cache, self.max_len = k, v, new_len
@@ -226,6 +227,32 @@ class BatchedGPT2:
         self.L = T
         lg = self._logits(h[:, -1])
         return lg.expand(B, -1).contiguous()
+
+    @torch.no_grad()
+    def forward_sequences(self, ids: torch.Tensor) -> torch.Tensor:
+        """Causal forward of B right-padded sequences ``[B, T]`` with positions ``0..T-1`` and no cache (the
+        guard's scoring pass, ``metrics/lm_scorer.py:121-131``); returns ``[B, T, ld]`` logits in
+        ``logits_dtype``.  Padding only follows the real tokens, so causality keeps it out of their rows."""
+        s = self.shape
+        B, T = ids.shape
+        if T > s.n_positions:
+            raise ValueError(f"sequence longer than n_positions ({s.n_positions})")
+        H, C = s.n_head, s.n_embd
+        D = C // H
+        pos = torch.arange(T, device=self.device)
+        h = self.wte[ids.to(self.device).long()] + self.wpe[pos][None]
+        for lw in self.layers:
+            a = self._ln(h, lw["ln1_w"], lw["ln1_b"])
+            qkv = torch.addmm(lw["qkv_b"], a.reshape(B * T, C), lw["qkv_w"]).view(B, T, 3, H, D)
+            q, k, v = (qkv[:, :, j].transpose(1, 2) for j in range(3))
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B * T, C)
+            h = h + torch.addmm(lw["o_b"], o, lw["o_w"]).view(B, T, C)
+            m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
+            f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B * T, C), lw["fc_w"]), approximate="tanh")
+            h = h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, T, C)
+        out = self._ln(h, self.lnf_w, self.lnf_b).reshape(B * T, C) @ self.head
+        out = out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
+        return out.view(B, T, self.ld)
 
     @torch.no_grad()
     def step(self, tokens: torch.Tensor) -> torch.Tensor:
