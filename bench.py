@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
     ap.add_argument("--e2e-batch", type=int, default=4096)
-    ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium"])
+    ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
                     help="logits handed to the coder; the fp16 head GEMM's output either way (f32 = upcast copy)")

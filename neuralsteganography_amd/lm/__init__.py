@@ -40,7 +40,7 @@ def load_lm(name: str, *, device: Optional[str] = None, logits_dtype: str = "f32
         from .gpt2 import random_gpt2
 
         base = name_norm[: -len("-random")]
-        if base not in {"gpt2", "gpt2-medium"}:
+        if base not in {"gpt2", "gpt2-medium", "gpt2-fa"}:
             raise ConfigurationError(f"unknown random-init architecture: {name}")
         return HipArithmeticLM(random_gpt2(base), None, device=device, logits_dtype=logits_dtype, **kwargs)
     if name_norm in {"gpt2", "gpt2-medium", "gpt2-fa"}:

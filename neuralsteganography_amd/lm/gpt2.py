@@ -276,6 +276,9 @@ def random_gpt2(name: str = "gpt2", *, seed: int = 1234, **overrides):
 
     sizes = {"gpt2": dict(n_layer=12, n_head=12, n_embd=768),
              "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),
+             # HooshvareLab/gpt2-fa (config C4): GPT-2-small geometry with its 42,001-id Persian vocabulary
+             # (unverified offline -- architecture only, random weights)
+             "gpt2-fa": dict(n_layer=12, n_head=12, n_embd=768, vocab_size=42001),
              "tiny": dict(n_layer=2, n_head=2, n_embd=64)}
     kw = dict(sizes[name])
     kw.update(overrides)
