@@ -154,12 +154,7 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, uint32_t* scr, int
     lds_fence();
     const uint4 c4 = reinterpret_cast<const uint4*>(scr)[lane];
     const uint32_t i1 = c4.x, i2 = i1 + c4.y, i3 = i2 + c4.z, i4 = i3 + c4.w;
-    uint32_t inc = i4;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
-        if (lane >= off) inc += y;
-    }
+    const uint32_t inc = wave_incl_scan_u32(i4);
     const uint32_t ex = inc - i4;
     // the bucket holding the K-th key: A < K <= A + C (exactly one, since cnt >= K)
     int hit = -1;
@@ -193,7 +188,7 @@ __device__ __noinline__ uint64_t compact_topk(uint64_t* keys, uint32_t* scr, int
     int r = 0;
     for (uint32_t t = 0; t < hstar; ++t) r += g[t] > mine ? 1 : 0;  // LDS broadcast reads
     const uint64_t mk = ballot(lane < (int)hstar && r == need - 1);
-    const uint64_t kappa = __shfl(mine, (int)__builtin_ctzll(mk));
+    const uint64_t kappa = readlane64(mine, (int)__builtin_ctzll(mk));
     // in-place keep: slot s's keys are read before any write, and writes land below (s+1)*64
     int base = 0;
 #pragma unroll 4
@@ -357,12 +352,7 @@ __device__ __forceinline__ bool bucket_rank(uint64_t* keys, uint32_t* base, cons
     lds_fence();
     const uint4 c4 = reinterpret_cast<const uint4*>(base)[lane];
     const uint32_t i1 = c4.x, i2 = i1 + c4.y, i3 = i2 + c4.z, i4 = i3 + c4.w;
-    uint32_t inc = i4;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
-        if (lane >= off) inc += y;
-    }
+    const uint32_t inc = wave_incl_scan_u32(i4);
     const uint32_t ex = inc - i4;
     reinterpret_cast<uint4*>(base)[lane] = make_uint4(ex, ex + i1, ex + i2, ex + i3);
     if (lane == 0) base[NB] = (uint32_t)K;
@@ -455,7 +445,7 @@ __device__ __forceinline__ void sample_tail(const StepParams& p, int b, const ns
         const int64_t q = (s < nsk && i < ks) ? (int64_t)__builtin_rint((e[s] / E) * SAMPLE_SCALE) : 0;
         const int64_t c = (s < nsk) ? wave_incl_scan(q, lane) + carry : carry;
         cum[s] = c;
-        if (s < nsk) carry = __shfl(c, WAVE - 1);
+        if (s < nsk) carry = (int64_t)readlane64((uint64_t)c, WAVE - 1);
     }
     const uint64_t total = (uint64_t)carry;
     const uint64_t u = rand64(p.seed, p.stream_offset + b, st.ntokens);
@@ -472,7 +462,7 @@ __device__ __forceinline__ void sample_tail(const StepParams& p, int b, const ns
     uint64_t tk = 0;
 #pragma unroll
     for (int s = 0; s < NSK; ++s)
-        if (s == sel / WAVE) tk = __shfl(sk[s], sel % WAVE);
+        if (s == sel / WAVE) tk = readlane64(sk[s], sel % WAVE);
     const int32_t token = (int32_t)key_id(tk);
     double kl = 0.0, h = 0.0;
     if (stats) {
@@ -751,7 +741,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
 
     NSG_STAMP(p, b, lane, 6);
     // ---------------- CDF step (canonical float64) ----------------
-    const double m = (double)key_val(__shfl(sk[0], 0));
+    const double m = (double)key_val(readlane64(sk[0], 0));
     double e[NSK];
 #pragma unroll
     for (int s = 0; s < NSK; ++s) {
@@ -851,7 +841,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         int64_t c = (s < nsk) ? wave_incl_scan(q, lane) + carry : carry;
         cum[s] = c;
         if (s < nsk) {
-            carry = __shfl(c, WAVE - 1);
+            carry = (int64_t)readlane64((uint64_t)c, WAVE - 1);
             const uint64_t mo = ballot(i < k && c > (int64_t)R);
             if (mo && kp == k) kp = s * WAVE + __builtin_ctzll(mo);
         }
@@ -861,7 +851,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         const int si = i / WAVE, li = i % WAVE;
 #pragma unroll
         for (int s = 0; s < NSK; ++s)
-            if (s == si) val = __shfl(cum[s], li);
+            if (s == si) val = (int64_t)readlane64((uint64_t)cum[s], li);
         return val;
     };
     const int64_t shift = (int64_t)R - cum_at(kp - 1) + (int64_t)st.lo;  // deficit + lo
@@ -920,7 +910,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         const int si = sel / WAVE, li = sel % WAVE;
 #pragma unroll
         for (int s = 0; s < NSK; ++s)
-            if (s == si) tk = __shfl(sk[s], li);
+            if (s == si) tk = readlane64(sk[s], li);
         token = (int32_t)key_id(tk);
     }
 

@@ -93,18 +93,57 @@ __device__ __forceinline__ double wave_sum_butterfly(double v) {
     for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+// DPP cross-lane steps (no LDS round trip, unlike ds_bpermute): row_shr:1,2,4,8 inside each 16-lane row,
+// then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- the wave64 inclusive scan of GFX9.  Lanes
+// whose source is outside the row keep `old` (the identity).  Exact for integer add and for max.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v, uint32_t identity) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += dpp_u32<0x111, 0xF>(v, 0u);
+    v += dpp_u32<0x112, 0xF>(v, 0u);
+    v += dpp_u32<0x114, 0xF>(v, 0u);
+    v += dpp_u32<0x118, 0xF>(v, 0u);
+    v += dpp_u32<0x142, 0xA>(v, 0u);
+    v += dpp_u32<0x143, 0xC>(v, 0u);
     return v;
 }
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int64_t dpp_add64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)u, 0u);
+    const uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)(u >> 32), 0u);
+    return v + (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        const int64_t y = __shfl_up(v, off);
-        if (lane >= off) v += y;
-    }
+    (void)lane;
+    v = dpp_add64<0x111, 0xF>(v);
+    v = dpp_add64<0x112, 0xF>(v);
+    v = dpp_add64<0x114, 0xF>(v);
+    v = dpp_add64<0x118, 0xF>(v);
+    v = dpp_add64<0x142, 0xA>(v);
+    v = dpp_add64<0x143, 0xC>(v);
     return v;
+}
+// value of lane `src` (wave-uniform) in every lane: two v_readlane, no LDS
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int src) {
+    src = __builtin_amdgcn_readfirstlane(src);  // the callers' lane index is uniform (ballot-derived)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    // max-scan with identity -inf, then lane 63 holds the wave max
+    const uint32_t ninf = 0xFF800000u;
+    auto step = [&](uint32_t o) { v = fmaxf(v, __uint_as_float(o)); };
+    step(dpp_u32<0x111, 0xF>(__float_as_uint(v), ninf));
+    step(dpp_u32<0x112, 0xF>(__float_as_uint(v), ninf));
+    step(dpp_u32<0x114, 0xF>(__float_as_uint(v), ninf));
+    step(dpp_u32<0x118, 0xF>(__float_as_uint(v), ninf));
+    step(dpp_u32<0x142, 0xA>(__float_as_uint(v), ninf));
+    step(dpp_u32<0x143, 0xC>(__float_as_uint(v), ninf));
+    return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(v), 63));
 }
 
 // ------------------------------------------------------------------------------------------------
