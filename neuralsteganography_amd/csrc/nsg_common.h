@@ -87,12 +87,7 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ void lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ double wave_sum_butterfly(double v) {
-    // canonical xor butterfly 32,16,8,4,2,1 (commutative per pair => every lane ends identical)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
-    return v;
-}
+
 // DPP cross-lane steps (no LDS round trip, unlike ds_bpermute): row_shr:1,2,4,8 inside each 16-lane row,
 // then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- the wave64 inclusive scan of GFX9.  Lanes
 // whose source is outside the row keep `old` (the identity).  Exact for integer add and for max.
@@ -124,6 +119,46 @@ __device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
     v = dpp_add64<0x118, 0xF>(v);
     v = dpp_add64<0x142, 0xA>(v);
     v = dpp_add64<0x143, 0xC>(v);
+    return v;
+}
+// value of lane (lane ^ OFF) without an LDS round trip: quad_perm for 1 and 2, row_shl/row_shr:4 selected by
+// lane bit 2, row_ror:8, and the gfx950 v_permlane16/32_swap for 16 and 32 (they return {vdst', vsrc'}: the
+// partner row sits in vsrc' for the lower row of each pair and in vdst' for the upper one)
+template <int OFF>
+__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t v) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if constexpr (OFF == 1) {
+        return dpp_u32<0xB1, 0xF>(v, 0u);
+    } else if constexpr (OFF == 2) {
+        return dpp_u32<0x4E, 0xF>(v, 0u);
+    } else if constexpr (OFF == 4) {
+        const uint32_t up = dpp_u32<0x104, 0xF>(v, 0u), dn = dpp_u32<0x114, 0xF>(v, 0u);
+        return (lane & 4u) ? dn : up;
+    } else if constexpr (OFF == 8) {
+        return dpp_u32<0x128, 0xF>(v, 0u);
+    } else if constexpr (OFF == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else {
+        static_assert(OFF == 32, "xor offsets 1..32");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    }
+}
+template <int OFF>
+__device__ __forceinline__ double xor_lane_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t w = ((uint64_t)xor_lane_u32<OFF>((uint32_t)(u >> 32)) << 32) | xor_lane_u32<OFF>((uint32_t)u);
+    return __builtin_bit_cast(double, w);
+}
+__device__ __forceinline__ double wave_sum_butterfly(double v) {
+    // canonical xor butterfly 32,16,8,4,2,1 (commutative per pair => every lane ends identical)
+    v = v + xor_lane_f64<32>(v);
+    v = v + xor_lane_f64<16>(v);
+    v = v + xor_lane_f64<8>(v);
+    v = v + xor_lane_f64<4>(v);
+    v = v + xor_lane_f64<2>(v);
+    v = v + xor_lane_f64<1>(v);
     return v;
 }
 // value of lane `src` (wave-uniform) in every lane: two v_readlane, no LDS
