@@ -31,6 +31,13 @@ int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, 
                         int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0, void* d_out,
                         int64_t out_stride, float scale, void* hip_stream);
 
+/* The same with the cache length read from device memory (*d_L0, int32) when the kernel runs, so one captured
+ * hipGraph serves every decode step; `cap` = the cache capacity in positions (a step with *d_L0 >= cap writes
+ * and reads nothing). */
+int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                            int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, const int32_t* d_L0,
+                            int cap, void* d_out, int64_t out_stride, float scale, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,8 @@ NS_MAX_BANNED = 8
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
-           "ns_read_counters", "ns_decode_attention", "ns_score_rows")
+           "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev",
+           "ns_score_rows")
 
 
 class NsStreamState(ctypes.Structure):
@@ -113,6 +114,10 @@ def lib() -> ctypes.CDLL:
     L.ns_read_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.ns_score_rows.restype = ctypes.c_int
     L.ns_score_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]
+    L.ns_decode_attention_dev.restype = ctypes.c_int
+    L.ns_decode_attention_dev.argtypes = [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int64,
+                                          ctypes.c_float, vp]
     L.ns_decode_attention.restype = ctypes.c_int
     L.ns_decode_attention.argtypes = [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_float, vp]

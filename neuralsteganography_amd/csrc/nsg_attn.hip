@@ -43,8 +43,11 @@ __device__ __forceinline__ void unpack8(f16x8 v, float* f) {
 __global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Float16* __restrict__ qkv,
                                                                      int64_t qkv_stride, _Float16* kc, _Float16* vc,
                                                                      int64_t cb, int64_t ch, int B, int H, int L0,
+                                                                     const int32_t* __restrict__ L0p, int cap,
                                                                      _Float16* __restrict__ out, int64_t out_stride,
                                                                      float scale_log2) {
+    if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
+    if (L0 < 0 || L0 >= cap) return;                     // never write past the cache (host checks capacity)
     const int lane = threadIdx.x & 63;
     const int pair = blockIdx.x * ATT_WAVES + (threadIdx.x >> 6);
     if (pair >= B * H) return;
@@ -137,22 +140,41 @@ __global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Floa
 
 }  // namespace nsg
 
-extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
-                                   int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
-                                   void* d_out, int64_t out_stride, float scale, void* hip_stream) {
+static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                            int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
+                            const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
+                            void* hip_stream) {
     if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0) return NS_ERR_CONFIG;
     if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
     const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_k_cache | (uintptr_t)d_v_cache | (uintptr_t)d_out;
     if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || (cache_b_stride & 7) || (cache_h_stride & 7))
         return NS_ERR_CONFIG;  // 16-byte rows
     if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
-    if (cache_h_stride < (int64_t)(L0 + 1) * D || cache_b_stride < (int64_t)H * cache_h_stride) return NS_ERR_CONFIG;
+    if (cache_h_stride < (int64_t)(L0 + 1) * D || cache_h_stride < (int64_t)cap * D ||
+        cache_b_stride < (int64_t)H * cache_h_stride)
+        return NS_ERR_CONFIG;
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
     const float scale_log2 = scale * 1.4426950408889634f;
     hipLaunchKernelGGL(nsg::decode_attn_kernel, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
                        dim3(64 * nsg::ATT_WAVES), 0, (hipStream_t)hip_stream, (const _Float16*)d_qkv, qkv_stride,
-                       (_Float16*)d_k_cache, (_Float16*)d_v_cache, cache_b_stride, cache_h_stride, B, H, L0,
-                       (_Float16*)d_out, out_stride, scale_log2);
+                       (_Float16*)d_k_cache, (_Float16*)d_v_cache, cache_b_stride, cache_h_stride, B, H, L0, d_L0,
+                       cap, (_Float16*)d_out, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                                   int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
+                                   void* d_out, int64_t out_stride, float scale, void* hip_stream) {
+    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, B, H, D, L0,
+                            nullptr, L0 + 1, d_out, out_stride, scale, hip_stream);
+}
+
+extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                                       int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D,
+                                       const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
+                                       void* hip_stream) {
+    if (!d_L0 || cap < 1) return NS_ERR_CONFIG;
+    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, B, H, D, 0,
+                            d_L0, cap, d_out, out_stride, scale, hip_stream);
 }

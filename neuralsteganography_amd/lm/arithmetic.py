@@ -74,6 +74,38 @@ class ByteTokenizer:
         return bytes(int(i) % 256 for i in ids).decode("utf-8", errors="ignore")
 
 
+class _StepGraph:
+    """One lockstep encode step -- the HIP coder step on the current logits, then the GPT-2 decode step that
+    turns its tokens into the next logits -- captured once as a hipGraph (``torch.cuda.CUDAGraph``) and replayed
+    per token.  Everything that changes per step lives on the device (coder state, token buffer, the cache
+    length ``d_L``), so a replay issues no host work besides the launch.  Construction runs one real step (on a
+    side stream, which also warms up every kernel and GEMM plan) before capturing the next."""
+
+    def __init__(self, lm, sess, logits, finish: bool):
+        import torch
+
+        self.lm, self.sess, self.finish = lm, sess, finish
+        self.logits = logits.clone()
+        lm.begin_static(self.logits)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._body()
+        torch.cuda.current_stream().wait_stream(side)
+        lm.L += 1
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._body()
+
+    def _body(self) -> None:
+        tok = self.sess.step(self.logits, finish_sent=self.finish)
+        self.lm.step_static(tok)
+
+    def replay(self) -> None:
+        self.graph.replay()
+        self.lm.L += 1
+
+
 class HipArithmeticLM:
     """Arithmetic-coding provider: batched GPT-2 on PyTorch-ROCm + the HIP coder step."""
 
@@ -189,8 +221,13 @@ class HipArithmeticLM:
     # ---------------------------------------------------------------- batched entry points
     def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], check_every: int = 16,
-                     stall_steps: int = 4096, return_stats: bool = False, stop_text: Optional[str] = None):
+                     stall_steps: int = 4096, return_stats: bool = False, stop_text: Optional[str] = None,
+                     graphs: bool = True):
         """Encode B independent bit lists in lockstep (one GPT-2 forward + one coder launch per token).
+
+        With ``graphs`` (and the HIP attention path) the per-token step is captured once as a hipGraph and
+        replayed, which removes the per-launch host cost that dominates at small batch; the cache budget
+        then bounds the replays and the loop continues eagerly (growing the cache) if it runs out.
 
         The reference coder has no underflow handling: when the interval straddles the midpoint and one
         token takes the whole range, no bit is ever fixed and ``code_base/arithmetic.py:114`` loops
@@ -213,6 +250,9 @@ class HipArithmeticLM:
         last_pos = None
         last_move = 0
         outs: List[List[int]] = [[] for _ in range(B)]
+        use_graph = (graphs and stop_text is None and getattr(self.lm, "hip_attention", False)
+                     and hasattr(self.lm, "begin_static"))
+        graph = None
         while True:
             if stop_text is not None and t > 0:
                 # code_base/arithmetic.py:207-210: a stream stops once its decoded cover text contains
@@ -246,9 +286,19 @@ class HipArithmeticLM:
                         f"streams {stuck[:8]} fixed no payload bit for {t - last_move} tokens: the interval "
                         "straddles the midpoint and one token takes the whole range (the reference coder "
                         "has no underflow handling and would loop forever)")
+            if use_graph and self.lm.static_capacity_left() >= 1:
+                if graph is None:
+                    graph = _StepGraph(self.lm, sess, logits, finish)
+                else:
+                    graph.replay()
+                t += 1
+                continue
+            if graph is not None:  # the preallocated cache is used up: continue eagerly (the cache grows)
+                logits, graph, use_graph = graph.logits, None, False
             tok = sess.step(logits, finish_sent=finish)
             logits = self.lm.step(tok)
             t += 1
+        del graph
         toks = sess.tokens()
         for b in bit_lists:
             st = _bits_count_state(len(b))

@@ -93,8 +93,11 @@ class BatchedGPT2:
             from .. import _lib
 
             self._attn = _lib.lib().ns_decode_attention
+            self._attn_dev = _lib.lib().ns_decode_attention_dev
             if self.shape.n_embd // self.shape.n_head != 64:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
+        self.d_L = None
+        self._static_logits = None
 
     # ------------------------------------------------------------------
     def kv_bytes_per_position(self, B: int) -> int:
@@ -171,8 +174,9 @@ class BatchedGPT2:
         h = h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, T, C)
         return h
 
-    def _block_decode_hip(self, i, h, a):
-        """One decode block with the fused KV-append + attention HIP kernel (``include/nsg_attn.h``)."""
+    def _block_decode_hip(self, i, h, a, dev_len: bool = False):
+        """One decode block with the fused KV-append + attention HIP kernel (``include/nsg_attn.h``); with
+        ``dev_len`` the cache length is read from ``self.d_L`` on the device (graph-capturable)."""
         from ..coder import _stream_handle
 
         s = self.shape
@@ -184,8 +188,13 @@ class BatchedGPT2:
         kc, vc = self.k_cache[i], self.v_cache[i]  # [Bmax, H, max_len, D]
         if self.L >= kc.shape[2]:
             raise RuntimeError("KV cache full")  # step() grows the cache before this point
-        rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
-                        B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), _stream_handle())
+        if dev_len:
+            rc = self._attn_dev(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                                kc.stride(1), B, H, D, self.d_L.data_ptr(), kc.shape[2], o.data_ptr(), o.stride(0),
+                                1.0 / math.sqrt(D), _stream_handle())
+        else:
+            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+                            B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), _stream_handle())
         if rc != 0:
             raise RuntimeError(f"ns_decode_attention failed ({rc})")
         h = h + torch.addmm(lw["o_b"], o, lw["o_w"]).view(B, 1, C)
@@ -253,6 +262,42 @@ class BatchedGPT2:
         out = self._ln(h, self.lnf_w, self.lnf_b).reshape(B * T, C) @ self.head
         out = out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
         return out.view(B, T, self.ld)
+
+    # ------------------------------------------------------------------ graph-capturable decode step
+    def begin_static(self, logits_out: torch.Tensor) -> None:
+        """Prepare :meth:`step_static`: the cache length moves to a device int32 (``d_L``) and the logits go to
+        the fixed buffer ``logits_out`` ([B, ld]), so the same captured hipGraph replays every decode step.
+        Needs the HIP attention path (fp16 on the GPU)."""
+        if not self.hip_attention:
+            raise RuntimeError("graph-captured decode steps need the HIP attention path (fp16 on the GPU)")
+        if logits_out.shape != (self.B, self.ld) or logits_out.dtype != self.logits_dtype:
+            raise ValueError(f"static logits must be [{self.B}, {self.ld}] {self.logits_dtype}")
+        self.d_L = torch.full((1,), self.L, dtype=torch.int32, device=self.device)
+        self._static_logits = logits_out
+
+    def static_capacity_left(self) -> int:
+        """Decode steps that still fit the preallocated cache (graph replays cannot grow it)."""
+        return self.max_len - self.L
+
+    @torch.no_grad()
+    def step_static(self, tokens: torch.Tensor) -> torch.Tensor:
+        """:meth:`step` with every per-step quantity on the device: position ``d_L % n_positions``, the
+        attention's cache length read from ``d_L``, logits written into the fixed buffer, ``d_L += 1``.  Issues
+        no host synchronisation and no allocation that depends on the step, so it can be captured once.  The
+        caller advances the host-side ``L`` by one per executed step."""
+        s = self.shape
+        pos = self.d_L.long() % s.n_positions
+        h = (self.wte.index_select(0, tokens.long()) + self.wpe.index_select(0, pos))[:, None, :]
+        for i in range(s.n_layer):
+            a = self._ln(h, self.layers[i]["ln1_w"], self.layers[i]["ln1_b"])
+            h = self._block_decode_hip(i, h, a, dev_len=True)
+        hf = self._ln(h[:, -1], self.lnf_w, self.lnf_b)
+        if self.logits_dtype == self.dtype:
+            torch.matmul(hf, self.head, out=self._static_logits)
+        else:
+            self._static_logits.copy_(hf @ self.head)
+        self.d_L += 1
+        return self._static_logits
 
     @torch.no_grad()
     def step(self, tokens: torch.Tensor) -> torch.Tensor:

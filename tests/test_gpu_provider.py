@@ -247,3 +247,25 @@ def test_gpt2_fp16_decode_hip_attention_matches_sdpa_and_hf():
     with torch.no_grad():
         ref = m(torch.tensor([seq])).logits[0, -1]
     assert (la[1, :50257].float().cpu() - ref).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("cap_extra", [None, 12])
+def test_graph_captured_encode_matches_eager(cap_extra):
+    """encode_batch with the per-token step captured as a hipGraph (coder + GPT-2 decode, cache length on the
+    device) gives the same tokens as the eager loop, including when the preallocated cache runs out and the
+    loop continues eagerly (cap_extra: cache limited to context + 12 positions)."""
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    m = random_gpt2("gpt2", seed=31)
+    q = {"temp": 0.9, "precision": 26, "topk": 300}
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 12)) for s in range(3)]
+    ctx = synthetic.DEFAULT_CONTEXT
+    out = {}
+    for graphs in (False, True):
+        lm = HipArithmeticLM(m, None, logits_dtype="f16")
+        if cap_extra is not None:
+            lm.lm.fit_positions = lambda B, want, reserve=0.15: len(ctx) + cap_extra
+        out[graphs] = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
+        assert lm.decode_batch(out[graphs], ctx, quality=q)[0][: len(bits[0])] == bits[0]
+    assert out[True] == out[False]
