@@ -346,6 +346,29 @@ class DecodeSession:
         self.ctx.check(rc, "ns_decode_step")
         self.t += 1
 
+    def step_static(self, logits, *, force_exact: bool = False):
+        """:meth:`step` with the token index on the device (``d_t``): the step's token / last / active rows are
+        gathered into fixed buffers by the device, so one captured hipGraph serves every step.  Returns the
+        token buffer (the LM's next input)."""
+        torch = _torch()
+        if getattr(self, "d_t", None) is None:
+            self.d_t = torch.full((1,), self.t, dtype=torch.long, device=self.state.device)
+            self.tok_s = torch.empty((1, self.B), dtype=self.tok.dtype, device=self.state.device)
+            self.last_s = torch.empty((1, self.B), dtype=self.last.dtype, device=self.state.device)
+            self.act_s = torch.empty((1, self.B), dtype=self.act.dtype, device=self.state.device)
+        torch.index_select(self.tok, 0, self.d_t, out=self.tok_s)
+        torch.index_select(self.last, 0, self.d_t, out=self.last_s)
+        torch.index_select(self.act, 0, self.d_t, out=self.act_s)
+        p = self.ctx.params
+        flags = _lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0
+        rc = _lib.lib().ns_decode_step(
+            self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok_s), _ptr(self.last_s),
+            _ptr(self.act_s), _ptr(self.state), _ptr(self.out_bits), self.out_stride, float(p.temp),
+            int(p.topk), self.ctx._banned, self.ctx._nbanned, _ptr(self.trace), flags, _stream_handle())
+        self.ctx.check(rc, "ns_decode_step")
+        self.d_t += 1
+        return self.tok_s[0]
+
     def bits(self) -> List[List[int]]:
         f = _state_fields(self.state)
         bad = np.nonzero(f["flags"] & _lib.NS_ST_ERR_DIVERGE)[0]

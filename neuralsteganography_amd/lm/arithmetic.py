@@ -81,10 +81,10 @@ class _StepGraph:
     length ``d_L``), so a replay issues no host work besides the launch.  Construction runs one real step (on a
     side stream, which also warms up every kernel and GEMM plan) before capturing the next."""
 
-    def __init__(self, lm, sess, logits, finish: bool):
+    def __init__(self, lm, coder_step, logits):
         import torch
 
-        self.lm, self.sess, self.finish = lm, sess, finish
+        self.lm, self.coder_step = lm, coder_step  # coder_step(logits) -> the step's token buffer [B] (device)
         self.logits = logits.clone()
         lm.begin_static(self.logits)
         side = torch.cuda.Stream()
@@ -98,8 +98,7 @@ class _StepGraph:
             self._body()
 
     def _body(self) -> None:
-        tok = self.sess.step(self.logits, finish_sent=self.finish)
-        self.lm.step_static(tok)
+        self.lm.step_static(self.coder_step(self.logits))
 
     def replay(self) -> None:
         self.graph.replay()
@@ -288,7 +287,7 @@ class HipArithmeticLM:
                         "has no underflow handling and would loop forever)")
             if use_graph and self.lm.static_capacity_left() >= 1:
                 if graph is None:
-                    graph = _StepGraph(self.lm, sess, logits, finish)
+                    graph = _StepGraph(self.lm, lambda lg: sess.step(lg, finish_sent=finish), logits)
                 else:
                     graph.replay()
                 t += 1
@@ -309,8 +308,9 @@ class HipArithmeticLM:
         return toks
 
     def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
-                     quality: Mapping[str, object]) -> List[List[int]]:
-        """Decode B token lists (ragged) in lockstep; returns every emitted bit (callers truncate)."""
+                     quality: Mapping[str, object], graphs: bool = True) -> List[List[int]]:
+        """Decode B token lists (ragged) in lockstep; returns every emitted bit (callers truncate).  With
+        ``graphs`` the per-token step (coder + GPT-2 decode) is a replayed hipGraph, as in :meth:`encode_batch`."""
         import torch
 
         from ..codec.errors import DecodeDivergenceError
@@ -325,6 +325,13 @@ class HipArithmeticLM:
         ctx = self._coder(params, B)
         sess = DecodeSession(ctx, token_lists)
         logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)
+        if (graphs and sess.T > 2 and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
+                and self.lm.static_capacity_left() >= sess.T):  # replays cannot grow the cache
+            graph = _StepGraph(self.lm, sess.step_static, logits)  # runs token 0, captures the next step
+            for _ in range(1, sess.T):  # the last replay's forward feeds nothing (the cache holds T + 1)
+                graph.replay()
+            del graph
+            return sess.bits()
         for t in range(sess.T):
             sess.step(logits)
             if t + 1 < sess.T:

@@ -267,5 +267,7 @@ def test_graph_captured_encode_matches_eager(cap_extra):
         if cap_extra is not None:
             lm.lm.fit_positions = lambda B, want, reserve=0.15: len(ctx) + cap_extra
         out[graphs] = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
-        assert lm.decode_batch(out[graphs], ctx, quality=q)[0][: len(bits[0])] == bits[0]
-    assert out[True] == out[False]
+        dec = lm.decode_batch(out[graphs], ctx, quality=q, graphs=graphs)
+        assert all(d[: len(b)] == b for d, b in zip(dec, bits))
+        out[("dec", graphs)] = dec
+    assert out[True] == out[False] and out[("dec", True)] == out[("dec", False)]
