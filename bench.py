@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
+    ap.add_argument("--blas", default=None, choices=["rocblas", "hipblaslt"],
+                    help="GEMM library for the GPT-2 forward (torch.backends.cuda.preferred_blas_library)")
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
                     help="logits handed to the coder; the fp16 head GEMM's output either way (f32 = upcast copy)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -107,6 +109,8 @@ def end_to_end(args, rank, world, dev):
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
     B = args.e2e_batch
+    if args.blas:
+        torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
                          max_batch=B)
     quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
