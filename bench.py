@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
+    ap.add_argument("--e2e-eager", action="store_true", help="per-token launches instead of the captured hipGraph")
     ap.add_argument("--blas", default=None, choices=["rocblas", "hipblaslt"],
                     help="GEMM library for the GPT-2 forward (torch.backends.cuda.preferred_blas_library)")
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
@@ -116,14 +117,14 @@ def end_to_end(args, rank, world, dev):
     quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
     context = synthetic.DEFAULT_CONTEXT
     # warm-up: GEMM heuristics, kernels and the coder context at the same batch, short payloads
-    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality)
+    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality, graphs=False if args.e2e_eager else None)
     mine = shard_range(B * world, world, rank)
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.e2e_payload_bytes)) for s in mine]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    toks = lm.encode_batch(bits, context, quality=quality)
+    toks = lm.encode_batch(bits, context, quality=quality, graphs=False if args.e2e_eager else None)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
