@@ -168,31 +168,49 @@ __global__ __launch_bounds__(256) void wide_collect_kernel(StepParams p, const W
     const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
     const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
     const int base_id = blockIdx.x * COLLECT_CHUNK;
+    // all loads first (NV in flight per lane), then ONE counter atomic per wave for the wave's whole chunk
+    // (the per-stream counter is shared by every block of the row: fewer atomics = less serialisation)
+    constexpr int NV = PER_THREAD / W;
+    float x[NV][W];
 #pragma unroll
-    for (int i = 0; i < PER_THREAD / W; ++i) {
+    for (int i = 0; i < NV; ++i) Elem<T>::unpack(rd.vec((base_id + (i * 256 + (int)threadIdx.x) * W) / W), x[i]);
+    uint64_t msk[NV][W];
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
         const int j0 = base_id + (i * 256 + (int)threadIdx.x) * W;
-        float x[W];
-        Elem<T>::unpack(rd.vec(j0 / W), x);
-        uint64_t msk[W];
-        int tot = 0;
 #pragma unroll
         for (int q = 0; q < W; ++q) {
             const int j = j0 + q;
-            const bool take = j < V && !is_banned(p, j) && x[q] >= xt;
-            msk[q] = ballot(take);
-            tot += popc64(msk[q]);
+            const bool take = j < V && !is_banned(p, j) && x[i][q] >= xt;
+            msk[i][q] = ballot(take);
+            tot += popc64(msk[i][q]);
         }
-        if (tot == 0) continue;
-        unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&count[b], (unsigned int)tot);
-        base = __shfl(base, 0);
-        int off = 0;
+    }
+    // one counter atomic per block: wave totals through LDS, wave bases = block base + earlier waves' totals
+    __shared__ unsigned int s_tot[256 / WAVE];
+    __shared__ unsigned int s_base;
+    const int wv = (int)threadIdx.x / WAVE;
+    if (lane == 0) s_tot[wv] = (unsigned int)tot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int all = 0;
+        for (int i = 0; i < 256 / WAVE; ++i) all += s_tot[i];
+        s_base = all ? atomicAdd(&count[b], all) : 0u;
+    }
+    __syncthreads();
+    if (tot == 0) return;
+    unsigned int base = s_base;
+    for (int i = 0; i < wv; ++i) base += s_tot[i];
+    int off = 0;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int j0 = base_id + (i * 256 + (int)threadIdx.x) * W;
 #pragma unroll
         for (int q = 0; q < W; ++q) {
-            const int j = j0 + q;
-            if ((msk[q] >> lane) & 1ull)
-                keys[(int64_t)b * cap + base + off + lanes_below(msk[q])] = wkey(x[q], (uint32_t)j);
-            off += popc64(msk[q]);
+            if ((msk[i][q] >> lane) & 1ull)
+                keys[(int64_t)b * cap + base + off + lanes_below(msk[i][q])] = wkey(x[i][q], (uint32_t)(j0 + q));
+            off += popc64(msk[i][q]);
         }
     }
 }
