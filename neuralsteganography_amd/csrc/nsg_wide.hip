@@ -480,26 +480,51 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     const int cs = (k + WIDE_THREADS - 1) / WIDE_THREADS;
     const int i0 = min(k, tid * cs), i1 = min(k, i0 + cs);
     auto q_of = [&](int i) -> int64_t { return (int64_t)__builtin_rint((e_of(i) / E) * Rd); };
+    // q of this thread's chunk computed once into registers when the chunk fits (k <= CQ * 1024, the usual
+    // case): the prefix, overfill, selection and cum passes below re-read them instead of re-evaluating
+    // exp_canon and re-loading the sorted keys each time
+    constexpr int CQ = 8;
+    const bool cached = cs <= CQ;
+    int64_t qc[CQ];
+#pragma unroll
+    for (int j = 0; j < CQ; ++j) qc[j] = (cached && i0 + j < i1) ? q_of(i0 + j) : 0;
+    auto for_chunk = [&](int iend, auto&& f) {  // f(rank, q) in rank order over [i0, iend); true = stop
+        if (cached) {
+#pragma unroll
+            for (int j = 0; j < CQ; ++j)
+                if (i0 + j < iend && f(i0 + j, qc[j])) return;
+        } else {
+            for (int i = i0; i < iend; ++i)
+                if (f(i, q_of(i))) return;
+        }
+    };
     int64_t local = 0;
-    for (int i = i0; i < i1; ++i) local += q_of(i);
+    for_chunk(i1, [&](int, int64_t q) {
+        local += q;
+        return false;
+    });
     int64_t total;
     const int64_t pre = block_excl_scan(local, sml, total);
     int kp_l = k;
     {
         int64_t c = pre;
-        for (int i = i0; i < i1; ++i) {
-            c += q_of(i);
+        for_chunk(i1, [&](int i, int64_t q) {
+            c += q;
             if (c > (int64_t)R) {
                 kp_l = i;
-                break;
+                return true;
             }
-        }
+            return false;
+        });
     }
     const int kp = block_min_int(kp_l, smi);
     // cum at rank kp-1 (its chunk owner recomputes the running prefix)
     auto cum_upto = [&](int i) -> int64_t {  // valid only for the owner of rank i
         int64_t c = pre;
-        for (int t = i0; t <= i; ++t) c += q_of(t);
+        for_chunk(i + 1, [&](int, int64_t q) {
+            c += q;
+            return false;
+        });
         return c;
     };
     if (kp - 1 >= i0 && kp - 1 < i1) cum_at[0] = cum_upto(kp - 1);
@@ -519,13 +544,14 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
             idx = (idx << 1) | bit;
         }
         int64_t c = pre;
-        for (int i = i0; i < min(i1, kp); ++i) {
-            c += q_of(i);
+        for_chunk(min(i1, kp), [&](int i, int64_t q) {
+            c += q;
             if ((uint64_t)(c + shift) > idx) {
                 sel_l = i;
-                break;
+                return true;
             }
-        }
+            return false;
+        });
     } else {
         const int32_t tok = p.in_token[b];
         if (tok >= 0 && tok < p.V && !is_banned(p, tok)) {
@@ -548,12 +574,12 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     double kl = 0.0;
     if (want_stats && !err) {
         const int64_t deficit = (int64_t)R - cum_at[0];
-        for (int i = i0; i < min(i1, kp); ++i) {
-            int64_t pf = q_of(i);
+        for_chunk(min(i1, kp), [&](int i, int64_t pf) {
             if (i == 0) pf += deficit;
             const double qd = (double)pf / Rd;
             if (qd > 0.0) kl += qd * (log(qd) - (((double)wkey_val(sk[i]) - m) - rs.lse1));
-        }
+            return false;
+        });
     }
     if (want_stats) kl = block_sum(kl, sm64);
     if (!err) {
