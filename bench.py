@@ -59,41 +59,34 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(pool_h, payload, nbits, args, seconds):
-    """The oracle port timed on one host core on a bounded sample of the same workload."""
-    from oracle import oracle
-    import ctypes
+def cpu_baseline(args, seconds, streams_per_core=16):
+    """The oracle port timed on the host cores on a bounded sample of the same workload (one
+    process per core, the core count from the affinity mask, capped at the box's 16-CPU share).  Each worker is
+    a child process (``python -m oracle.cpu_baseline``) that never touches the GPU and encodes its own streams
+    of 3·N(0,1) fp32 rows for ``seconds``; bits and stream-steps are summed, the time is the slowest worker's."""
+    import subprocess
 
-    L = oracle.lib()
-    V, P = args.vocab, args.precision
-    rows_all = pool_h  # list of [Bs, ld] float32
-    Bs = rows_all[0].shape[0]
-    ld = rows_all[0].shape[1]
-    banned = np.asarray([V - 1, 628], dtype=np.int32)
-    st = (oracle.OrState * Bs)()
-    for i in range(Bs):
-        L.or_init_state(ctypes.byref(st[i]), P)
-    out = np.zeros(Bs, np.int32)
-    pl = np.ascontiguousarray(payload[:Bs])
-    nb = np.ascontiguousarray(nbits[:Bs])
-    steps = 0
-    bits0 = sum(st[i].bit_pos for i in range(Bs))
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        rows = np.ascontiguousarray(rows_all[steps % len(rows_all)])
-        rc = L.or_encode_batch(rows.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ld, Bs, V,
-                               banned.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 2, 1.0 / args.temp, P,
-                               args.topk, pl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), pl.shape[1],
-                               nb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), st,
-                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
-        assert rc == 0
-        steps += 1
-    dt = time.perf_counter() - t0
-    bits = sum(st[i].bit_pos for i in range(Bs)) - bits0
-    return {"value": bits / dt, "unit": "payload bits/s", "cores": 1, "kind": "port",
-            "cover_tokens_per_s": steps * Bs / dt,
-            "sample": f"oracle/nsg_oracle.c or_encode_batch, {Bs} streams x {steps} steps of the same logit pool "
-                      f"({dt:.1f} s on 1 core)"}
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    procs = []
+    for c in range(cores):
+        cmd = [sys.executable, "-m", "oracle.cpu_baseline", str(seconds), str(streams_per_core), str(1000 + c),
+               str(args.vocab), str(args.temp), str(args.precision), str(args.topk), str(args.payload_bytes)]
+        procs.append(subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=subprocess.PIPE, text=True))
+    res = []
+    for pr in procs:
+        text, _ = pr.communicate(timeout=seconds * 4 + 120)
+        if pr.returncode != 0:
+            raise RuntimeError(f"cpu_baseline worker failed ({pr.returncode})")
+        res.append(json.loads(text.strip().splitlines()[-1]))
+    dt = max(r["seconds"] for r in res)
+    bits = sum(r["bits"] for r in res)
+    ss = sum(r["stream_steps"] for r in res)
+    return {"value": bits / dt, "unit": "payload bits/s", "cores": cores, "kind": "port",
+            "cover_tokens_per_s": ss / dt, "per_core_bits_per_s": bits / dt / cores,
+            "sample": f"oracle/nsg_oracle.c or_encode_batch: {cores} worker processes (1 core each) x "
+                      f"{streams_per_core} streams of 3N(0,1) fp32 rows, V {args.vocab}, topk {args.topk}, "
+                      f"{args.payload_bytes}-byte payloads, {dt:.1f} s"}
 
 
 def end_to_end(args, rank, world, dev):
@@ -270,23 +263,15 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None,
-                     "kernel": "coder_step_kernel<float,false>", "alg_bytes_per_launch": alg_bytes},
+                     "kernel": f"coder_step_kernel<{'_Float16' if args.dtype == 'f16' else 'float'},false>", "alg_bytes_per_launch": alg_bytes},
     }
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
-    Bs = 16
-    pool_h = [p[:Bs].float().cpu().numpy() for p in pool[:2]] if want_cpu else None
     del pool, sess, ctx
     torch.cuda.empty_cache()
     if not args.no_e2e:
         out["end_to_end"] = end_to_end(args, rank, world, dev)
     if want_cpu:
-        nb = np.asarray([len(b) for b in payload_bits], dtype=np.int64)
-        stride = int((nb.max() + 7) // 8)
-        pl = np.zeros((B, stride), np.uint8)
-        for i, b in enumerate(payload_bits[:64]):
-            pk = np.packbits(np.asarray(b, np.uint8), bitorder="little")
-            pl[i, : pk.size] = pk
-        out["cpu_baseline"] = cpu_baseline(pool_h, pl, nb, args, args.cpu_baseline_seconds)
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
