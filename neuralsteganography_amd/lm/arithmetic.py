@@ -249,15 +249,17 @@ class HipArithmeticLM:
         budget = 2 * max_bits + 64            # initial KV/history capacity (grows on demand)
         hard_cap = 64 * max_bits + 4096       # a stream fixing < 1/64 bit per token is reported, not looped
         logits = self.lm.prefill(context, B, budget)
-        sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap, stats=return_stats)
-        t = 0
-        last_pos = None
-        last_move = 0
-        outs: List[List[int]] = [[] for _ in range(B)]
         if graphs is None:
             graphs = B <= GRAPH_MAX_BATCH
         use_graph = (graphs and stop_text is None and getattr(self.lm, "hip_attention", False)
                      and hasattr(self.lm, "begin_static"))
+        # token history: a captured graph needs a fixed buffer (the hard cap); the eager loop starts at the
+        # KV budget and grows it at the host checks (at B = 4096 the hard cap alone would be 8.6 GB)
+        sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap if use_graph else budget, stats=return_stats)
+        t = 0
+        last_pos = None
+        last_move = 0
+        outs: List[List[int]] = [[] for _ in range(B)]
         graph = None
         while True:
             if stop_text is not None and t > 0:
@@ -277,6 +279,8 @@ class HipArithmeticLM:
                 f = sess.fields()
                 if bool((f["flags"] & 1).all()):
                     break
+                if graph is None:
+                    sess.ensure_history(check_every + 1)
                 pos = f["bit_pos"].copy()
                 if last_pos is None or (pos != last_pos).any():
                     last_pos, last_move = pos, t
