@@ -199,7 +199,8 @@ int ns_token_probs(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, double 
 /* Rare-event diagnostics, cumulative since ns_create: counters[0] = stream-steps that took the exact-sum
  * path, counters[1] = candidate-buffer overflow compactions, counters[2] = speculative-threshold misses
  * (row re-read), counters[3] = top-K selections that left the histogram fast path (value ties or a skewed
- * row: bisection compaction or full-count ranking).  Synchronises the device. */
+ * row: bisection compaction or full-count ranking; on the wide path, LDS sorts that fell back to bitonic
+ * order).  Synchronises the device. */
 int ns_read_counters(ns_ctx* ctx, uint64_t* host_counters4);
 
 #ifdef __cplusplus

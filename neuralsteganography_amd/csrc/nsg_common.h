@@ -395,6 +395,11 @@ struct RowReader {
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, NSG_LOAD_AUX);
         return make_uint4(r[0], r[1], r[2], r[3]);
     }
+    // default cache policy: bytes the same workgroup reads again soon (kept in L2 / the Infinity Cache)
+    __device__ __forceinline__ uint4 vec_keep(int v) const {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, 0);
+        return make_uint4(r[0], r[1], r[2], r[3]);
+    }
 };
 
 // Proven interval of the canonical float64 row sum S from the fast estimate S_r = sum 2^((x-r)*c32)

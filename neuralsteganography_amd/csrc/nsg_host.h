@@ -33,6 +33,7 @@ struct NsgWide {
     unsigned int* count = nullptr;  // [max_batch] collected ids per stream
     unsigned int* begin = nullptr;  // [max_batch] segment offsets for the sort
     unsigned int* end = nullptr;    // [max_batch]
+    unsigned int* todo = nullptr;   // [1 + max_batch] streams left to wide_cdf_kernel: count, then ids
     nsg::WideStat* stat = nullptr;  // [max_batch]
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;

@@ -5,9 +5,10 @@
 //   1. wide_stats_kernel   (wave per stream)  : one streaming pass -> row max, second max, fast-sum interval
 //   2. wide_collect_kernel (blocks per chunk) : every id that can clear the 1/R cutoff, plus the top two,
 //                                               written as 49-bit (value desc, id asc) keys to a segment
-//   3. rocprim::segmented_radix_sort_keys_desc : per-stream descending sort of the collected keys
-//   4. wide_cdf_kernel     (1024 threads/stream): cutoff, canonical sums, rint, int64 scan, overfill,
-//                                               selection, interval update
+//   3. wide_fast_kernel    (512 threads/stream): streams with <= 8,192 keys: LDS sort + the canonical tail
+//   4. rocprim::segmented_radix_sort_keys_desc : descending sort of the larger streams' keys
+//   5. wide_cdf_kernel     (1024 threads/stream): the other streams: cutoff, canonical sums, rint, int64 scan,
+//                                               overfill, selection, interval update
 // An id left out by step 2 has e_i < S_lo/R <= S/R, i.e. p_i < 1/R for certain, so the first rank below the
 // cutoff lies inside the collected prefix or right after it.
 
@@ -215,16 +216,31 @@ __global__ __launch_bounds__(256) void wide_collect_kernel(StepParams p, const W
     }
 }
 
+// segments for the device-wide sort: only the streams with more than `small` keys (the rest are sorted in LDS by
+// wide_fast_kernel; small = 0 sorts every segment)
 __global__ void wide_offsets_kernel(int B, int cap, const WideStat* ws, const unsigned int* count,
-                                    unsigned int* begin, unsigned int* end) {
+                                    unsigned int* begin, unsigned int* end, unsigned int small,
+                                    unsigned int* todo) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (todo && b == 0) todo[0] = 0u;
     if (b < B) {
+        const unsigned int n = ws[b].active ? count[b] : 0u;
         begin[b] = (unsigned int)(b * cap);
-        end[b] = (unsigned int)(b * cap) + (ws[b].active ? count[b] : 0u);
+        end[b] = (unsigned int)(b * cap) + (n > small ? n : 0u);
     }
 }
 
 // ------------------------------------------------------------------------------------------ pass 4
+// the next P payload bits (LSB-first bytes) as an MSB-first integer, zero-padded past the end: one bit per lane
+// and a ballot (every lane of the wave must be active); the loads are independent, not a P-long chain
+__device__ __forceinline__ uint64_t payload_window(const StepParams& p, int b, int64_t bit_pos) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int64_t bp = bit_pos + lane;
+    uint32_t bit = 0u;
+    if (lane < p.P && bp < p.nbits[b]) bit = (p.payload[(int64_t)b * p.payload_stride + (bp >> 3)] >> (bp & 7)) & 1u;
+    return __builtin_bitreverse64(ballot(bit != 0u)) >> (64 - p.P);
+}
+
 // block helpers (1024 threads = 16 waves)
 __device__ __forceinline__ int block_min_int(int v, int* sm) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -280,9 +296,20 @@ __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, dou
         }
         __syncthreads();
         if (threadIdx.x < 64) {
-            // groups of this round in increasing order: g = base/4 + g_local, lane = g & 63
+            // groups of this round in increasing order: g = base/4 + g_local, lane = g & 63; four groups' loads
+            // issued ahead of their (ordered) adds
             const int g0 = base / 4;
-            for (int gl = ((int)threadIdx.x - g0 % 64 + 64) % 64; gl < WIDE_ROUND / 4; gl += 64) {
+            int gl = ((int)threadIdx.x - g0 % 64 + 64) % 64;
+            for (; gl + 3 * 64 < WIDE_ROUND / 4; gl += 4 * 64) {
+                double t[16];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) t[4 * u + q] = ebuf[4 * (gl + 64 * u) + q];
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc += t[v];
+            }
+            for (; gl < WIDE_ROUND / 4; gl += 64) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc += ebuf[4 * gl + q];
             }
@@ -330,17 +357,69 @@ __device__ RowStats block_row_stats(const StepParams& p, const char* rowc, doubl
     return rs;
 }
 
+// interval update, bit emit and state/statistics writes of one finished step (thread 0; both CDF kernels)
+template <bool DECODE>
+__device__ __forceinline__ void wide_finish(const StepParams& p, int b, const ns_stream_state& st, int k, int kp, int sel, bool exact,
+                            double S_used, int64_t cum_m1, int64_t cum_sel, int64_t shift, uint64_t sel_key, double m,
+                            const RowStats& rs, double kl, bool want_stats) {
+    const int P = p.P;
+    const uint64_t mask = (P >= 64) ? ~0ull : ((1ull << P) - 1ull);
+    const uint64_t new_lo = sel > 0 ? (uint64_t)(cum_m1 + shift) : st.lo;
+    const uint64_t new_hi = (uint64_t)(cum_sel + shift);
+    const uint64_t top = new_hi - 1ull;
+    const uint64_t diff = (new_lo ^ top) & mask;
+    const int n = diff == 0ull ? P - 1 : P - (64 - __builtin_clzll(diff));
+    const int32_t token = (int32_t)wkey_id(sel_key);
+    ns_stream_state ns = st;
+    if (DECODE) {
+        const bool last = p.is_last[b] != 0;
+        const int cntb = last ? P : n;
+        const uint64_t src = last ? new_lo : top;
+        uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
+        for (int t = 0; t < cntb; ++t) {
+            const int64_t bp = st.bit_pos + t;
+            const uint8_t bitv = (uint8_t)((src >> (P - 1 - t)) & 1u);
+            const uint8_t bm = (uint8_t)(1u << (bp & 7));
+            ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | bm) : (uint8_t)(ob[bp >> 3] & ~bm);
+        }
+        ns.bit_pos = st.bit_pos + cntb;
+    } else {
+        ns.bit_pos = st.bit_pos + n;
+    }
+    ns.lo = (new_lo << n) & mask;
+    ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
+    ns.ntokens = st.ntokens + 1;
+    ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
+    if (!DECODE && ns.bit_pos >= p.nbits[b] && !(p.flags & NS_STEP_FINISH_SENT)) ns.flags |= NS_ST_DONE;
+    p.state[b] = ns;
+    if (!DECODE) {
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+    }
+    if (p.trace) {
+        ns_step_trace tr = {k, kp, sel, n, token, exact ? 1 : 0, S_used};
+        p.trace[b] = tr;
+    }
+    if (want_stats) {
+        double* a = p.stats + 4 * (int64_t)b;
+        a[0] += ((double)wkey_val(sel_key) - m) - rs.lse1;
+        a[1] += kl / 0.69315;
+        a[2] += (rs.lst - rs.a_over_s) / 0.69315;
+        a[3] += 1.0;
+    }
+    if (p.counters && exact) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1))], 1ull);
+}
+
+// the canonical tail of one stream (keys_sorted: its collected keys in rank order); every thread of the block
 template <typename T, bool DECODE>
-__global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, const WideStat* ws,
-                                                                const uint64_t* keys_sorted,
-                                                                const unsigned int* count, int cap) {
+__device__ __forceinline__ void wide_cdf_stream(const StepParams& p, const WideStat* ws, const uint64_t* keys_sorted,
+                                                const unsigned int* count, int cap, const int b) {
     __shared__ double ebuf[WIDE_ROUND];
     __shared__ double sm64[64];
     __shared__ int smi[16];
     __shared__ int64_t sml[16];
     __shared__ int64_t cum_at[4];  // [0] cum(kp-1), [1] cum(sel-1), [2] cum(sel)
     __shared__ uint64_t sel_key;
-    const int b = blockIdx.x;
     const WideStat w = ws[b];
     if (!w.active) return;
     const int tid = threadIdx.x;
@@ -535,14 +614,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
     int sel_l = 0x7FFFFFFF;
     uint32_t err = 0;
     if (!DECODE) {
-        uint64_t idx = 0;
-        const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
-        const int64_t nbits = p.nbits[b];
-        for (int t = 0; t < p.P; ++t) {
-            const int64_t bp = st.bit_pos + t;
-            const uint32_t bit = bp < nbits ? ((pl[bp >> 3] >> (bp & 7)) & 1u) : 0u;
-            idx = (idx << 1) | bit;
-        }
+        const uint64_t idx = payload_window(p, b, st.bit_pos);
         int64_t c = pre;
         for_chunk(min(i1, kp), [&](int i, int64_t q) {
             c += q;
@@ -597,52 +669,642 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
         }
         return;
     }
-    const int P = p.P;
-    const uint64_t mask = (P >= 64) ? ~0ull : ((1ull << P) - 1ull);
-    const uint64_t new_lo = sel > 0 ? (uint64_t)(cum_at[1] + shift) : st.lo;
-    const uint64_t new_hi = (uint64_t)(cum_at[2] + shift);
-    const uint64_t top = new_hi - 1ull;
-    const uint64_t diff = (new_lo ^ top) & mask;
-    const int n = diff == 0ull ? P - 1 : P - (64 - __builtin_clzll(diff));
-    const int32_t token = (int32_t)wkey_id(sel_key);
-    ns_stream_state ns = st;
-    if (DECODE) {
-        const bool last = p.is_last[b] != 0;
-        const int cntb = last ? P : n;
-        const uint64_t src = last ? new_lo : top;
-        uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
-        for (int t = 0; t < cntb; ++t) {
-            const int64_t bp = st.bit_pos + t;
-            const uint8_t bitv = (uint8_t)((src >> (P - 1 - t)) & 1u);
-            const uint8_t bm = (uint8_t)(1u << (bp & 7));
-            ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | bm) : (uint8_t)(ob[bp >> 3] & ~bm);
+    wide_finish<DECODE>(p, b, st, k, kp, sel, exact, S_used, cum_at[1], cum_at[2], shift, sel_key, m, rs, kl,
+                        want_stats);
+}
+
+// the streams wide_fast_kernel listed (todo[1 .. todo[0]]: more keys than its LDS holds, or a step it hands on),
+// a grid-stride loop over the list so that the launch does not depend on how many there are
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, const WideStat* ws,
+                                                                const uint64_t* keys_sorted,
+                                                                const unsigned int* count, int cap,
+                                                                const unsigned int* todo) {
+    const unsigned int nt = todo[0];
+    for (unsigned int i = blockIdx.x; i < nt; i += gridDim.x) {
+        wide_cdf_stream<T, DECODE>(p, ws, keys_sorted, count, cap, (int)todo[1 + i]);
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------ passes 3+4 in LDS
+// The usual stream keeps a few thousand ids (3·N(0,1) logits at precision 16: 2-5k), far fewer than the
+// device-wide sort is sized for.  One 512-thread workgroup per such stream (count <= FAST_NL) sorts its keys in
+// LDS -- a counting sort on FAST_NB key-range buckets, then each key's rank inside its bucket by counting the
+// larger bucket-mates (a bitonic sort instead when a bucket holds more than FAST_OCC_MAX keys) -- and runs the
+// canonical tail on the sorted keys: the same arithmetic, in the same order, as wide_cdf_kernel.  Streams that
+// need the exact row sum, the row-statistics fallback, the sampler, or hit an error are handed to
+// wide_cdf_kernel (listed in todo) with their sorted keys written to keys_out; streams with more keys were
+// sorted by the device-wide sort and are listed too.  80,896 B of LDS: two workgroups per CU.
+constexpr int FAST_THREADS = 512;
+constexpr int FAST_WAVES = FAST_THREADS / WAVE;
+constexpr int FAST_NL = 8192;                      // keys of a stream sorted in LDS
+constexpr int FAST_R = FAST_NL / FAST_THREADS;     // ranks per thread: rank i = r * FAST_THREADS + tid
+constexpr int FAST_NB = 3840;                      // counting-sort buckets over [kmin, kmax]
+constexpr uint32_t FAST_OCC_MAX = 48;              // fuller bucket -> bitonic sort
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int off) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int wave_min_int(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+    return v;
+}
+
+// the LDS path for one stream whose n <= FAST_NL collected keys sit at `kin` (global or LDS, any order): sort,
+// then the canonical tail; every thread of the 512-thread block calls it
+template <typename T, bool DECODE>
+__device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w, const int b, const int n,
+                                          const uint64_t* kin, uint64_t* keys_out, const int cap, unsigned int* todo,
+                                          uint64_t* s_keys, uint64_t* s_aux) {
+    uint32_t* s_cnt = (uint32_t*)s_aux;
+    const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    // ---- load (unsorted, as collected) + key range
+    uint64_t kr[FAST_R];
+    uint64_t kmax = 0ull, kmin = ~0ull;
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        const int i = r * FAST_THREADS + tid;
+        kr[r] = i < n ? kin[i] : 0ull;
+        if (i < n) {
+            kmax = kr[r] > kmax ? kr[r] : kmax;
+            kmin = kr[r] < kmin ? kr[r] : kmin;
         }
-        ns.bit_pos = st.bit_pos + cntb;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t a = shfl_xor_u64(kmax, off), c = shfl_xor_u64(kmin, off);
+        kmax = a > kmax ? a : kmax;
+        kmin = c < kmin ? c : kmin;
+    }
+    if (lane == 0) {
+        s_aux[wv] = kmax;
+        s_aux[FAST_WAVES + wv] = kmin;
+    }
+    __syncthreads();
+    uint64_t hi = s_aux[0], lo = s_aux[FAST_WAVES];
+#pragma unroll
+    for (int i = 1; i < FAST_WAVES; ++i) {
+        hi = s_aux[i] > hi ? s_aux[i] : hi;
+        lo = s_aux[FAST_WAVES + i] < lo ? s_aux[FAST_WAVES + i] : lo;
+    }
+    __syncthreads();
+    for (int i = tid; i < FAST_NB; i += FAST_THREADS) s_cnt[i] = 0u;
+    __syncthreads();
+    // ---- counting sort: bucket 0 = the largest keys (monotone: a larger key never gets a later bucket)
+    const double bscale = (double)FAST_NB / ((double)(hi - lo) + 1.0);
+    uint32_t bs[FAST_R];  // bucket << 16 | slot inside the bucket
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        const int i = r * FAST_THREADS + tid;
+        bs[r] = 0u;
+        if (i < n) {
+            const uint32_t bk = min((uint32_t)((double)(hi - kr[r]) * bscale), (uint32_t)(FAST_NB - 1));
+            bs[r] = (bk << 16) | atomicAdd(&s_cnt[bk], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* scr = (uint32_t*)s_keys;  // wave totals (s_keys is free until the scatter)
+    uint32_t occ = 0u;
+    {
+        constexpr int PER = (FAST_NB + FAST_THREADS - 1) / FAST_THREADS;  // 8 buckets per thread
+        const int c0 = tid * PER;
+        uint32_t loc[PER], sum = 0u, mx = 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            loc[j] = c0 + j < FAST_NB ? s_cnt[c0 + j] : 0u;
+            sum += loc[j];
+            mx = max(mx, loc[j]);
+        }
+        const uint32_t inc = wave_incl_scan_u32(sum);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        if (lane == WAVE - 1) scr[wv] = inc;
+        if (lane == 0) scr[FAST_WAVES + wv] = mx;
+        __syncthreads();
+        uint32_t run = inc - sum;
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) {
+            if (i < wv) run += scr[i];
+            occ = max(occ, scr[FAST_WAVES + i]);
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (c0 + j < FAST_NB) {
+                s_cnt[c0 + j] = run;
+                run += loc[j];
+            }
+    }
+    __syncthreads();
+    const bool bitonic = occ > FAST_OCC_MAX;
+    if (bitonic && tid == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 3], 1ull);
+    int P2 = 1;
+    while (P2 < n) P2 <<= 1;
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        const int i = r * FAST_THREADS + tid;
+        if (i < n) s_keys[s_cnt[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = kr[r];
+    }
+    if (bitonic)
+        for (int i = n + tid; i < P2; i += FAST_THREADS) s_keys[i] = 0ull;  // below every real key
+    __syncthreads();
+    if (!bitonic) {
+        // rank = bucket start + larger keys in the bucket (keys are distinct: ids are)
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (i < n) {
+                const uint32_t bk = bs[r] >> 16;
+                const uint32_t s0 = s_cnt[bk], s1 = bk + 1 < (uint32_t)FAST_NB ? s_cnt[bk + 1] : (uint32_t)n;
+                uint32_t c = s0;
+                for (uint32_t j = s0; j < s1; ++j) c += s_keys[j] > kr[r] ? 1u : 0u;
+                bs[r] = c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (i < n) s_keys[bs[r]] = kr[r];
+        }
+        __syncthreads();
     } else {
-        ns.bit_pos = st.bit_pos + n;
+        for (int size = 2; size <= P2; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int t = tid; t < P2 / 2; t += FAST_THREADS) {
+                    const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+                    const uint64_t a = s_keys[i], c = s_keys[j];
+                    if ((a < c) == ((i & size) == 0)) {
+                        s_keys[i] = c;
+                        s_keys[j] = a;
+                    }
+                }
+                __syncthreads();
+            }
     }
-    ns.lo = (new_lo << n) & mask;
-    ns.hi = (((top << n) & mask) | ((1ull << n) - 1ull)) + 1ull;
-    ns.ntokens = st.ntokens + 1;
-    ns.flags = (st.flags & ~NS_ST_EXACT_SUM) | (exact ? NS_ST_EXACT_SUM : 0u);
-    if (!DECODE && ns.bit_pos >= p.nbits[b] && !(p.flags & NS_STEP_FINISH_SENT)) ns.flags |= NS_ST_DONE;
-    p.state[b] = ns;
+    // ---- sorted keys of this thread's ranks into registers; s_keys becomes the e_i array
+    uint64_t ks[FAST_R];
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        const int i = r * FAST_THREADS + tid;
+        ks[r] = i < n ? s_keys[i] : 0ull;
+    }
+    const uint64_t top = s_keys[0];
+    __syncthreads();
+    auto defer = [&]() __attribute__((always_inline)) {  // hand the stream to wide_cdf_kernel with its keys in rank order
+        uint64_t* ko = keys_out + (int64_t)b * cap;
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (i < n) ko[i] = ks[r];
+        }
+        if (tid == 0) todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
+    };
+    const ns_stream_state st = p.state[b];
+    const double m = (double)wkey_val(top);
+    const bool want_stats = !DECODE && p.stats != nullptr;
+    RowStats rs{0.0, 0.0, 0.0};
+    if ((!DECODE && p.sample) || w.exact ||
+        (want_stats && !row_stats_from_stream(w.S_r, w.B_r, w.U_r, w.r, m, p.inv_temp, rs))) {
+        defer();
+        return;
+    }
+    const int Kc = min(n, p.K);
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R;
+    const double thr = 1.0 / Rd;
+    double* s_e = (double*)s_keys;
+    // ---- 1. cutoff k0 (the fast-sum interval decides it, or the stream needs the exact sum)
+    int fb = Kc, fa = Kc;
+    {
+        const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15));
+        const double inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (i < Kc) {
+                const double e = exp_canon(((double)wkey_val(ks[r]) - m) * p.inv_temp);
+                s_e[i] = e;
+                const bool below = e * inv_lo < thr;
+                const bool above = e * inv_hi >= thr;
+                if (below) fb = min(fb, i);
+                if (!below && !above) fa = min(fa, i);
+            }
+        }
+    }
+    int* s_i = (int*)(s_aux + 16);
+    fb = wave_min_int(fb);
+    fa = wave_min_int(fa);
+    if (lane == 0) {
+        s_i[wv] = fb;
+        s_i[FAST_WAVES + wv] = fa;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) {
+        fb = min(fb, s_i[i]);
+        fa = min(fa, s_i[FAST_WAVES + i]);
+    }
+    int k = fb < 2 ? 2 : fb;
+    if (k > p.topk) k = p.topk;
+    if (fa < fb || k > Kc) {  // ambiguous cutoff (exact row sum) or a degenerate row: wide_cdf_kernel
+        defer();
+        return;
+    }
+    // ---- 2. E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
+    double* s_d = (double*)(s_aux + 32);
+    if (wv == 0) {
+        double acc = 0.0;
+        int i = lane;
+        for (; i + 7 * WAVE < k; i += 8 * WAVE) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = s_e[i + u * WAVE];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += t[u];
+        }
+        for (; i < k; i += WAVE) acc += s_e[i];
+        acc = wave_sum_butterfly(acc);
+        if (lane == 0) s_d[0] = acc;
+    }
+    __syncthreads();
+    const double E = s_d[0];
+    // ---- 3. q_i = rint(e_i/E*R); inclusive prefix in rank order (wave scans + per-round wave totals)
+    const int nr = (k + FAST_THREADS - 1) / FAST_THREADS;
+    int64_t* s_tot = (int64_t*)(s_aux + 64);  // [FAST_R][FAST_WAVES]
+    int64_t cum[FAST_R];
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        cum[r] = 0;
+        if (r < nr) {
+            const int i = r * FAST_THREADS + tid;
+            const int64_t q = i < k ? (int64_t)__builtin_rint((s_e[i] / E) * Rd) : 0;
+            cum[r] = wave_incl_scan(q, lane);
+            if (lane == WAVE - 1) s_tot[r * FAST_WAVES + wv] = cum[r];
+        }
+    }
+    __syncthreads();
+    {
+        int64_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r)
+            if (r < nr) {
+                int64_t before = 0, all = 0;
+#pragma unroll
+                for (int j = 0; j < FAST_WAVES; ++j) {
+                    const int64_t t = s_tot[r * FAST_WAVES + j];
+                    if (j < wv) before += t;
+                    all += t;
+                }
+                cum[r] += carry + before;
+                carry += all;
+            }
+    }
+    // overfill: kp = first rank whose cum exceeds R
+    int kp = k;
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        const int i = r * FAST_THREADS + tid;
+        if (r < nr && i < k && cum[r] > (int64_t)R) kp = min(kp, i);
+    }
+    int* s_j = (int*)(s_aux + 256);
+    kp = wave_min_int(kp);
+    if (lane == 0) s_j[wv] = kp;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) kp = min(kp, s_j[i]);
+    int64_t* s_c = (int64_t*)(s_aux + 272);  // [0] cum(kp-1), [1] cum(sel-1), [2] cum(sel), [3] key(sel)
+    auto publish = [&](int rank, int slot, bool key) __attribute__((always_inline)) {  // owner of `rank` writes its cum (or key) to s_c[slot]
+        if (rank >= 0 && rank % FAST_THREADS == tid) {
+            // masked sum, not `if (r == rr)`: the compiler folds that into an indexed load, which puts the
+            // register arrays in scratch memory
+            const int rr = rank / FAST_THREADS;
+            int64_t v = 0;
+#pragma unroll
+            for (int r = 0; r < FAST_R; ++r) v |= (key ? (int64_t)ks[r] : cum[r]) & -(int64_t)(r == rr);
+            s_c[slot] = v;
+        }
+    };
+    publish(kp - 1, 0, false);
+    __syncthreads();
+    const int64_t cum_kp = s_c[0];
+    const int64_t shift = (int64_t)R - cum_kp + (int64_t)st.lo;
+    // ---- selection
+    int sel = 0x7FFFFFFF;
     if (!DECODE) {
-        p.out_token[b] = token;
-        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        const uint64_t idx = payload_window(p, b, st.bit_pos);
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (r < nr && i < kp && (uint64_t)(cum[r] + shift) > idx) sel = min(sel, i);
+        }
+    } else {
+        const int32_t tok = p.in_token[b];
+        if (tok >= 0 && tok < p.V && !is_banned(p, tok)) {
+            const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+            const uint64_t kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+#pragma unroll
+            for (int r = 0; r < FAST_R; ++r) {
+                const int i = r * FAST_THREADS + tid;
+                if (i < kp && ks[r] == kt) sel = min(sel, i);
+            }
+        }
     }
-    if (p.trace) {
-        ns_step_trace tr = {k, kp, sel, n, token, exact ? 1 : 0, S_used};
-        p.trace[b] = tr;
+    int* s_k = (int*)(s_aux + 288);
+    sel = wave_min_int(sel);
+    if (lane == 0) s_k[wv] = sel;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) sel = min(sel, s_k[i]);
+    if (sel == 0x7FFFFFFF) {  // range / divergence error: wide_cdf_kernel reports it (and the ranked export)
+        defer();
+        return;
     }
+    publish(sel - 1, 1, false);
+    publish(sel, 2, false);
+    publish(sel, 3, true);
+    // statistics of an encode step (arithmetic.py:193-199): KL(q || p) over the k' kept entries
+    double kl = 0.0;
     if (want_stats) {
-        double* a = p.stats + 4 * (int64_t)b;
-        a[0] += ((double)wkey_val(sel_key) - m) - rs.lse1;
-        a[1] += kl / 0.69315;
-        a[2] += (rs.lst - rs.a_over_s) / 0.69315;
-        a[3] += 1.0;
+        const int64_t deficit = (int64_t)R - cum_kp;
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (r < nr && i < kp) {
+                int64_t pf = (int64_t)__builtin_rint((s_e[i] / E) * Rd);
+                if (i == 0) pf += deficit;
+                const double qd = (double)pf / Rd;
+                if (qd > 0.0) kl += qd * (log(qd) - (((double)wkey_val(ks[r]) - m) - rs.lse1));
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) kl += __shfl_xor(kl, off);
+        if (lane == 0) s_d[8 + wv] = kl;
     }
-    if (p.counters && exact) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1))], 1ull);
+    __syncthreads();
+    if (tid != 0) return;
+    if (want_stats) {
+        kl = 0.0;
+        for (int i = 0; i < FAST_WAVES; ++i) kl += s_d[8 + i];
+    }
+    wide_finish<DECODE>(p, b, st, k, kp, sel, false, w.S_fast, s_c[1], s_c[2], shift, (uint64_t)s_c[3], m, rs, kl,
+                        want_stats);
+}
+
+
+// ------------------------------------------------------------------------------------------ fused wide step
+// One 512-thread workgroup per stream does passes 1 and 2 and, for the usual stream, the whole step:
+//   pass 1: stream the row once (default cache policy) -> max, second max, the proven fast-sum interval
+//           (fp32 groups of W terms, as wide_stats_kernel: the same bound)
+//   pass 2: stream it again -- two workgroups per CU keep ~512 rows (~100 MB fp32) in flight, so the re-read
+//           comes from the Infinity Cache, not HBM -- collecting the ids that can clear the cutoff into LDS
+//   then fast_tail (LDS sort + canonical tail).  More than FAST_NL keys: pass 3 writes them to keys_in for the
+//   device-wide sort and the stream is listed for wide_cdf_kernel.
+__device__ __forceinline__ float uni_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ double uni_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+                                                                   uint64_t* keys_out, unsigned int* count, int cap,
+                                                                   unsigned int* todo) {
+    __shared__ uint64_t s_keys[FAST_NL];
+    __shared__ uint64_t s_aux[FAST_NB / 2];
+    constexpr int W = Elem<T>::W;
+    constexpr int G = 16 / W;                 // vectors in flight per thread (64 B)
+    constexpr int TS = FAST_THREADS * W;      // ids per block-wide vector row
+    const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    const ns_stream_state st = p.state[b];
+    bool active = !(st.flags & NS_ST_DONE);
+    if (!DECODE && !p.sample && active && st.bit_pos >= p.nbits[b]) {
+        if (tid == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
+        active = false;
+    }
+    if (DECODE && p.active && !p.active[b]) active = false;
+    if (!active) {
+        if (tid == 0) {
+            ws[b].active = 0;
+            count[b] = 0;
+        }
+        return;
+    }
+    const int V = p.V;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int nvec = (V + W - 1) / W;
+    const int nsup = (nvec + G * FAST_THREADS - 1) / (G * FAST_THREADS);
+    // x[g][.] = block-row (s*G + g) of this thread; ids >= V and banned ids -> `fill` (pass 1: -inf, which adds
+    // nothing to the sums; pass 2: NaN, which no threshold collects -- a real -inf logit is a valid id and is
+    // collected when the threshold is -inf, as in wide_collect_kernel)
+    auto load_group = [&](int sI, float (&x)[G][W], int& bi, int& next_ban, bool keep,
+                          float fill) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int v = (sI * G + g) * FAST_THREADS + tid;
+            Elem<T>::unpack(keep ? rd.vec_keep(v) : rd.vec(v), x[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = ((sI * G + g) * FAST_THREADS + tid) * W;
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (j0 + q >= V) x[g][q] = fill;
+            while (next_ban < (sI * G + g + 1) * TS) {
+#pragma unroll
+                for (int q = 0; q < W; ++q)
+                    if (j0 + q == next_ban) x[g][q] = fill;
+                ++bi;
+                next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+            }
+        }
+    };
+    // ---- pass 1
+    float r = 0.0f, m1 = -__builtin_inff(), m2 = -__builtin_inff();
+    double acc64 = 0.0, b64 = 0.0, u64 = 0.0;
+    const bool stats = p.stats != nullptr;
+    {
+        int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        for (int sI = 0; sI < nsup; ++sI) {
+            float x[G][W];
+            load_group(sI, x, bi, next_ban, true, -__builtin_inff());
+            if (sI == 0) {  // reference r = max of the first block rows (any finite reference is valid)
+                float mx = -__builtin_inff();
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int q = 0; q < W; ++q) mx = fmaxf(mx, x[g][q]);
+                mx = wave_max(mx);
+                float* s_f = (float*)(s_aux + 8);
+                if (lane == 0) s_f[wv] = mx;
+                __syncthreads();
+                r = s_f[0];
+#pragma unroll
+                for (int i = 1; i < FAST_WAVES; ++i) r = fmaxf(r, s_f[i]);
+                if (r == -__builtin_inff()) r = 0.0f;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float a = 0.0f, bb = 0.0f, uu = 0.0f;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    const float dx = fmaxf(x[g][q] - r, -3.0e38f);
+                    const float e = __builtin_amdgcn_exp2f(dx * p.c32);
+                    a += e;
+                    if (stats) {
+                        bb += e * dx;
+                        uu += __builtin_amdgcn_exp2f(dx * L2E_F);
+                    }
+                    m2 = fmaxf(m2, fminf(m1, x[g][q]));
+                    m1 = fmaxf(m1, x[g][q]);
+                }
+                acc64 += (double)a;
+                b64 += (double)bb;
+                u64 += (double)uu;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
+        m2 = fmaxf(fminf(m1, o1), fmaxf(m2, o2));
+        m1 = fmaxf(m1, o1);
+    }
+    acc64 = wave_sum_butterfly(acc64);
+    b64 = wave_sum_butterfly(b64);
+    u64 = wave_sum_butterfly(u64);
+    {
+        double* s_d = (double*)(s_aux + 16);  // [3][FAST_WAVES]
+        float* s_f = (float*)(s_aux + 48);    // [2][FAST_WAVES]
+        if (lane == 0) {
+            s_d[wv] = acc64;
+            s_d[FAST_WAVES + wv] = b64;
+            s_d[2 * FAST_WAVES + wv] = u64;
+            s_f[wv] = m1;
+            s_f[FAST_WAVES + wv] = m2;
+        }
+        __syncthreads();
+        acc64 = b64 = u64 = 0.0;
+        m1 = m2 = -__builtin_inff();
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) {
+            acc64 += s_d[i];
+            b64 += s_d[FAST_WAVES + i];
+            u64 += s_d[2 * FAST_WAVES + i];
+            const float o1 = s_f[i], o2 = s_f[FAST_WAVES + i];
+            m2 = fmaxf(fminf(m1, o1), fmaxf(m2, o2));
+            m1 = fmaxf(m1, o1);
+        }
+    }
+    // block-uniform from here on: into scalar registers (the LDS tail needs the vector registers)
+    acc64 = uni_f64(acc64);
+    b64 = uni_f64(b64);
+    u64 = uni_f64(u64);
+    m1 = uni_f32(m1);
+    m2 = uni_f32(m2);
+    WideStat w;
+    {
+        double Sf = 0.0, S_lo = 0.0, S_hi = 0.0;
+        const bool ok = fast_sum_interval(acc64, r, (double)(m1 + 0.0f), p.c32, p.inv_temp, W, Sf, S_lo, S_hi);
+        w.m = m1;
+        w.m2 = m2;
+        w.r = r;
+        w.active = 1;
+        w.S_lo = S_lo;
+        w.S_hi = S_hi;
+        w.S_fast = Sf;
+        w.exact = (ok && !(p.flags & NS_STEP_FORCE_EXACT_SUM)) ? 0u : 1u;
+        w.pad = 0;
+        w.S_r = acc64;
+        w.B_r = b64;
+        w.U_r = u64;
+        w.S_lo = uni_f64(w.S_lo);
+        w.S_hi = uni_f64(w.S_hi);
+        w.S_fast = uni_f64(w.S_fast);
+        w.exact = (uint32_t)__builtin_amdgcn_readfirstlane((int)w.exact);
+    }
+    if (tid == 0) ws[b] = w;
+    // ---- collection threshold (as wide_collect_kernel)
+    float xt;
+    {
+        const double thr = 1.0 / (double)(st.hi - st.lo);
+        const double temp = 1.0 / p.inv_temp;
+        if (p.sample) {
+            const double t = (double)w.m - temp * 41.58883083359672;
+            xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + temp * 41.58883083359672));
+        } else if (w.exact) {
+            xt = -__builtin_inff();
+        } else {
+            const double L = log(w.S_lo * thr);
+            const double t = (double)w.m + temp * L;
+            xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + fabs(temp * L)));
+        }
+        xt = uni_f32(fminf(xt, w.m2));  // at least the top two ids (k >= 2)
+    }
+    // ---- pass 2 (and pass 3 into global memory when the keys overflow the LDS)
+    uint32_t* s_ctr = (uint32_t*)(s_aux + FAST_NB / 2 - 1);
+    if (tid == 0) s_ctr[0] = 0u;
+    __syncthreads();
+    auto collect = [&](bool to_global) __attribute__((always_inline)) {
+        uint64_t* kout = keys_in + (int64_t)b * cap;
+        int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        for (int sI = 0; sI < nsup; ++sI) {
+            float x[G][W];
+            load_group(sI, x, bi, next_ban, false, __builtin_nanf(""));
+            uint32_t tot = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int q = 0; q < W; ++q) tot += (uint32_t)popc64(ballot(x[g][q] >= xt));
+            if (tot == 0u) continue;  // wave-uniform
+            uint32_t base = 0u;
+            if (lane == 0) base = atomicAdd(s_ctr, tot);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+            uint32_t off = 0u;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int j0 = ((sI * G + g) * FAST_THREADS + tid) * W;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    const uint64_t mk = ballot(x[g][q] >= xt);  // recomputed: cheaper than holding G*W masks
+                    const uint32_t pos = base + off + (uint32_t)lanes_below(mk);
+                    if ((mk >> lane) & 1ull) {
+                        const uint64_t key = wkey(x[g][q], (uint32_t)(j0 + q));
+                        if (to_global) {
+                            if (pos < (uint32_t)cap) kout[pos] = key;  // n <= V - nbanned <= cap
+                        }
+                        else if (pos < (uint32_t)FAST_NL)
+                            s_keys[pos] = key;
+                    }
+                    off += (uint32_t)popc64(mk);
+                }
+            }
+        }
+    };
+    collect(false);
+    __syncthreads();
+    const int n = (int)s_ctr[0];
+    if (n <= FAST_NL) {
+        if (tid == 0) count[b] = (unsigned int)n;
+        fast_tail<T, DECODE>(p, w, b, n, s_keys, keys_out, cap, todo, s_keys, s_aux);
+        return;
+    }
+    __syncthreads();
+    if (tid == 0) s_ctr[0] = 0u;
+    __syncthreads();
+    collect(true);
+    if (tid == 0) {
+        count[b] = (unsigned int)n;
+        todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
+    }
 }
 
 // ------------------------------------------------------------------------------------------ rank coder
@@ -881,6 +1543,7 @@ int nsg_wide_alloc(ns_ctx* ctx) {
         hipMalloc((void**)&w.count, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.begin, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.end, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void**)&w.todo, (ctx->max_batch + 1) * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.stat, ctx->max_batch * sizeof(nsg::WideStat)) != hipSuccess)
         return NS_ERR_HIP;
     size_t bytes = 0;
@@ -895,7 +1558,7 @@ int nsg_wide_alloc(ns_ctx* ctx) {
 void nsg_wide_free(ns_ctx* ctx) {
     NsgWide& w = ctx->wide;
     for (void* ptr : {(void*)w.keys_in, (void*)w.keys_out, (void*)w.count, (void*)w.begin, (void*)w.end,
-                      (void*)w.stat, w.sort_tmp})
+                      (void*)w.todo, (void*)w.stat, w.sort_tmp})
         if (ptr) (void)hipFree(ptr);
     w = NsgWide();
 }
@@ -904,20 +1567,18 @@ template <typename T, bool DECODE>
 static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
     NsgWide& w = ctx->wide;
     const int B = p.B;
-    hipLaunchKernelGGL((nsg::wide_stats_kernel<T, DECODE>), dim3((B + nsg::WPB - 1) / nsg::WPB),
-                       dim3(nsg::WPB * nsg::WAVE), 0, s, p, w.stat, w.count);
-    const int nchunk = (p.V + nsg::COLLECT_CHUNK - 1) / nsg::COLLECT_CHUNK;
-    hipLaunchKernelGGL((nsg::wide_collect_kernel<T>), dim3(nchunk, B), dim3(256), 0, s, p, w.stat, w.keys_in,
-                       w.count, w.cap);
+    if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
+    hipLaunchKernelGGL((nsg::wide_scan_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
+                       w.keys_in, w.keys_out, w.count, w.cap, w.todo);
     hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
-                       w.count, w.begin, w.end);
+                       w.count, w.begin, w.end, (unsigned int)nsg::FAST_NL, nullptr);
     size_t bytes = w.sort_tmp_bytes;
     if (rocprim::segmented_radix_sort_keys_desc(w.sort_tmp, bytes, w.keys_in, w.keys_out,
                                                 (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin,
                                                 w.end, 0, 49, s) != hipSuccess)
         return false;
-    hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B), dim3(nsg::WIDE_THREADS), 0, s, p, w.stat,
-                       w.keys_out, w.count, w.cap);
+    hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B < 256 ? B : 256), dim3(nsg::WIDE_THREADS), 0, s, p,
+                       w.stat, w.keys_out, w.count, w.cap, w.todo);
     return hipGetLastError() == hipSuccess;
 }
 
@@ -931,7 +1592,7 @@ static bool rank_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     hipLaunchKernelGGL((nsg::wide_collect_kernel<T>), dim3(nchunk, B), dim3(256), 0, s, p, w.stat, w.keys_in,
                        w.count, w.cap);
     hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
-                       w.count, w.begin, w.end);
+                       w.count, w.begin, w.end, 0u, nullptr);
     size_t bytes = w.sort_tmp_bytes;
     if (rocprim::segmented_radix_sort_keys_desc(w.sort_tmp, bytes, w.keys_in, w.keys_out,
                                                 (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin,

@@ -277,3 +277,50 @@ def test_adversarial_rows_exercise_fallback_paths(mode):
         assert c1[1] > c0[1], "overflow compaction path was not exercised"
     else:
         assert c1[3] > c0[3], "slow top-K selection path was not exercised"
+
+
+@pytest.mark.parametrize("mode", ["plain", "ties", "outlier", "mixed"])
+def test_wide_lds_path_matches_oracle(mode):
+    """The wide path's LDS sort (streams with <= 8,192 collected keys, api defaults precision 16 / topk 50,000):
+    'plain' rows keep 2-5k keys (counting sort + in-bucket ranks), 'ties' quantises the logits so a few values
+    hold thousands of keys each (over-full buckets -> bitonic sort), 'outlier' leaves the top two keys only (every other step),
+    'mixed' puts streams of all three kinds and a flat row (> 8,192 keys: the device-wide sort) in one batch.
+    Tokens must match the oracle and decode back to the payload."""
+    from neuralsteganography_amd.coder import CoderParams, decode_batch, encode_batch, row_stride
+
+    torch = _torch()
+    V, B = 50257, 4
+    params = CoderParams(vocab=V, precision=16, temp=1.0, topk=50000)
+    ctx = _ctx(params, B)
+    assert ctx.wide
+    ld = row_stride(V, "f32")
+    kinds = {"plain": ["plain"] * B, "ties": ["ties"] * B, "outlier": ["outlier"] * B,
+             "mixed": ["plain", "ties", "outlier", "flat"]}[mode]
+
+    def row(s, t):
+        kind = kinds[s]
+        x = synthetic.logits_row(91, s, t, V, 0.5 if kind == "flat" else 3.0)
+        if kind == "ties":
+            x = np.round(x * 2.0) / 2.0
+        elif kind == "outlier" and t % 2 == 0:  # (every step would carry no bits at all)
+            x[(97 * t + 13 * s) % (V - 2)] = 3.0e30
+        return x.astype(np.float32)
+
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 6)) for s in range(B)]
+    expect = [oracle.encode_stream(lambda t, s=s: row(s, t), bits[s], banned=params.banned_ids(), temp=1.0,
+                                   precision=16, topk=50000)[0] for s in range(B)]
+
+    def fn(t, _last=None):
+        arr = np.zeros((B, ld), np.float32)
+        for s in range(B):
+            arr[s, :V] = row(s, t)
+        return torch.from_numpy(arr).cuda()
+
+    c0 = ctx.counters()
+    toks = encode_batch(ctx, bits, fn)
+    assert toks == expect
+    if "ties" in kinds:
+        assert ctx.counters()[3] > c0[3], "the bitonic fallback of the LDS sort was not exercised"
+    got = decode_batch(ctx, toks, fn)
+    for s in range(B):
+        assert got[s][: len(bits[s])] == bits[s]

@@ -40,6 +40,7 @@ def main():
     for t in range(3):
         sess.step(pool[t % 3])
     torch.cuda.synchronize()
+    c0 = ctx.counters()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     for t in range(a.steps):
         ev[t][0].record()
@@ -49,7 +50,8 @@ def main():
     ms = float(np.mean([x.elapsed_time(y) for x, y in ev]))
     sess.raise_errors()
     print(json.dumps({"lib": Path(_lib.LIB_PATH).name, "batch": B, "topk": a.topk, "precision": a.precision,
-                      "ms_per_step": round(ms, 4), "tokens": int(sess.fields()["ntokens"].sum())}), flush=True)
+                      "ms_per_step": round(ms, 4), "tokens": int(sess.fields()["ntokens"].sum()),
+                      "exact_sum_steps": ctx.counters()[0] - c0[0], "stream_steps": B * a.steps}), flush=True)
 
 
 if __name__ == "__main__":
