@@ -696,6 +696,12 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 // need the exact row sum, the row-statistics fallback, the sampler, or hit an error are handed to
 // wide_cdf_kernel (listed in todo) with their sorted keys written to keys_out; streams with more keys were
 // sorted by the device-wide sort and are listed too.  80,896 B of LDS: two workgroups per CU.
+#ifndef NSG_SCAN_DIAG
+#define NSG_SCAN_DIAG 0
+#endif
+#ifndef NSG_SCAN_P1_KEEP
+#define NSG_SCAN_P1_KEEP 1  // pass 1 loads with the default policy (0: non-temporal, for A/B timing)
+#endif
 constexpr int FAST_THREADS = 512;
 constexpr int FAST_WAVES = FAST_THREADS / WAVE;
 constexpr int FAST_NL = 8192;                      // keys of a stream sorted in LDS
@@ -854,6 +860,10 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     }
     const uint64_t top = s_keys[0];
     __syncthreads();
+#if NSG_SCAN_DIAG == 3  // passes 1 and 2 and the LDS sort only
+    if (tid == 0) atomicExch((unsigned int*)&keys_out[(int64_t)b * cap], (unsigned int)ks[0]);  // keep ks live
+    return;
+#endif
     auto defer = [&]() __attribute__((always_inline)) {  // hand the stream to wide_cdf_kernel with its keys in rank order
         uint64_t* ko = keys_out + (int64_t)b * cap;
 #pragma unroll
@@ -910,7 +920,9 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     }
     int k = fb < 2 ? 2 : fb;
     if (k > p.topk) k = p.topk;
-    if (fa < fb || k > Kc) {  // ambiguous cutoff (exact row sum) or a degenerate row: wide_cdf_kernel
+    // ambiguous cutoff (the exact row sum: measured cheaper in the list kernel than in this one, whose
+    // workgroup slots are the row stream's) or a degenerate row: wide_cdf_kernel
+    if (fa < fb || k > Kc) {
         defer();
         return;
     }
@@ -1105,15 +1117,18 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
     // x[g][.] = block-row (s*G + g) of this thread; ids >= V and banned ids -> `fill` (pass 1: -inf, which adds
     // nothing to the sums; pass 2: NaN, which no threshold collects -- a real -inf logit is a valid id and is
     // collected when the threshold is -inf, as in wide_collect_kernel)
-    auto load_group = [&](int sI, float (&x)[G][W], int& bi, int& next_ban, bool keep,
-                          float fill) __attribute__((always_inline)) {
+    auto fetch = [&](int sI, uint4 (&raw)[G], bool keep) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int v = (sI * G + g) * FAST_THREADS + tid;
-            Elem<T>::unpack(keep ? rd.vec_keep(v) : rd.vec(v), x[g]);
+            raw[g] = keep ? rd.vec_keep(v) : rd.vec(v);
         }
+    };
+    auto prep = [&](int sI, const uint4 (&raw)[G], float (&x)[G][W], int& bi, int& next_ban,
+                    float fill) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
+            Elem<T>::unpack(raw[g], x[g]);
             const int j0 = ((sI * G + g) * FAST_THREADS + tid) * W;
 #pragma unroll
             for (int q = 0; q < W; ++q)
@@ -1127,51 +1142,67 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
             }
         }
     };
+    // one sweep over the row: consume(sI, x) for every block row in order, the loads of block row sI + 1 in
+    // flight while block row sI is consumed (two register buffers, no copies between them)
+    auto sweep = [&](bool keep, float fill, auto&& consume) __attribute__((always_inline)) {
+        int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        uint4 ra[G], rb[G];
+        fetch(0, ra, keep);
+        for (int sI = 0; sI < nsup; sI += 2) {
+            if (sI + 1 < nsup) fetch(sI + 1, rb, keep);
+            {
+                float x[G][W];
+                prep(sI, ra, x, bi, next_ban, fill);
+                consume(sI, x);
+            }
+            if (sI + 1 < nsup) {
+                if (sI + 2 < nsup) fetch(sI + 2, ra, keep);
+                float x[G][W];
+                prep(sI + 1, rb, x, bi, next_ban, fill);
+                consume(sI + 1, x);
+            }
+        }
+    };
     // ---- pass 1
     float r = 0.0f, m1 = -__builtin_inff(), m2 = -__builtin_inff();
     double acc64 = 0.0, b64 = 0.0, u64 = 0.0;
     const bool stats = p.stats != nullptr;
-    {
-        int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
-        for (int sI = 0; sI < nsup; ++sI) {
-            float x[G][W];
-            load_group(sI, x, bi, next_ban, true, -__builtin_inff());
-            if (sI == 0) {  // reference r = max of the first block rows (any finite reference is valid)
-                float mx = -__builtin_inff();
+    sweep(NSG_SCAN_P1_KEEP != 0, -__builtin_inff(), [&](int sI, float (&x)[G][W]) __attribute__((always_inline)) {
+        if (sI == 0) {  // reference r = max of the first block rows (any finite reference is valid)
+            float mx = -__builtin_inff();
 #pragma unroll
-                for (int g = 0; g < G; ++g)
+            for (int g = 0; g < G; ++g)
 #pragma unroll
-                    for (int q = 0; q < W; ++q) mx = fmaxf(mx, x[g][q]);
-                mx = wave_max(mx);
-                float* s_f = (float*)(s_aux + 8);
-                if (lane == 0) s_f[wv] = mx;
-                __syncthreads();
-                r = s_f[0];
+                for (int q = 0; q < W; ++q) mx = fmaxf(mx, x[g][q]);
+            mx = wave_max(mx);
+            float* s_f = (float*)(s_aux + 8);
+            if (lane == 0) s_f[wv] = mx;
+            __syncthreads();
+            r = s_f[0];
 #pragma unroll
-                for (int i = 1; i < FAST_WAVES; ++i) r = fmaxf(r, s_f[i]);
-                if (r == -__builtin_inff()) r = 0.0f;
-            }
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float a = 0.0f, bb = 0.0f, uu = 0.0f;
-#pragma unroll
-                for (int q = 0; q < W; ++q) {
-                    const float dx = fmaxf(x[g][q] - r, -3.0e38f);
-                    const float e = __builtin_amdgcn_exp2f(dx * p.c32);
-                    a += e;
-                    if (stats) {
-                        bb += e * dx;
-                        uu += __builtin_amdgcn_exp2f(dx * L2E_F);
-                    }
-                    m2 = fmaxf(m2, fminf(m1, x[g][q]));
-                    m1 = fmaxf(m1, x[g][q]);
-                }
-                acc64 += (double)a;
-                b64 += (double)bb;
-                u64 += (double)uu;
-            }
+            for (int i = 1; i < FAST_WAVES; ++i) r = fmaxf(r, s_f[i]);
+            if (r == -__builtin_inff()) r = 0.0f;
         }
-    }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float a = 0.0f, bb = 0.0f, uu = 0.0f;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const float dx = fmaxf(x[g][q] - r, -3.0e38f);
+                const float e = __builtin_amdgcn_exp2f(dx * p.c32);
+                a += e;
+                if (stats) {
+                    bb += e * dx;
+                    uu += __builtin_amdgcn_exp2f(dx * L2E_F);
+                }
+                m2 = fmaxf(m2, fminf(m1, x[g][q]));
+                m1 = fmaxf(m1, x[g][q]);
+            }
+            acc64 += (double)a;
+            b64 += (double)bb;
+            u64 += (double)uu;
+        }
+    });
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const float o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
@@ -1232,6 +1263,10 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
         w.exact = (uint32_t)__builtin_amdgcn_readfirstlane((int)w.exact);
     }
     if (tid == 0) ws[b] = w;
+#if NSG_SCAN_DIAG == 1  // timing diagnostics (tools/wide_timing.py on a tools/build_variant.sh build): pass 1 only
+    if (tid == 0) count[b] = 0u;
+    return;
+#endif
     // ---- collection threshold (as wide_collect_kernel)
     float xt;
     {
@@ -1255,16 +1290,13 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
     __syncthreads();
     auto collect = [&](bool to_global) __attribute__((always_inline)) {
         uint64_t* kout = keys_in + (int64_t)b * cap;
-        int bi = 0, next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
-        for (int sI = 0; sI < nsup; ++sI) {
-            float x[G][W];
-            load_group(sI, x, bi, next_ban, false, __builtin_nanf(""));
+        sweep(false, __builtin_nanf(""), [&](int sI, float (&x)[G][W]) __attribute__((always_inline)) {
             uint32_t tot = 0;
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int q = 0; q < W; ++q) tot += (uint32_t)popc64(ballot(x[g][q] >= xt));
-            if (tot == 0u) continue;  // wave-uniform
+            if (tot == 0u) return;  // wave-uniform
             uint32_t base = 0u;
             if (lane == 0) base = atomicAdd(s_ctr, tot);
             base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
@@ -1280,18 +1312,22 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
                         const uint64_t key = wkey(x[g][q], (uint32_t)(j0 + q));
                         if (to_global) {
                             if (pos < (uint32_t)cap) kout[pos] = key;  // n <= V - nbanned <= cap
-                        }
-                        else if (pos < (uint32_t)FAST_NL)
+                        } else if (pos < (uint32_t)FAST_NL) {
                             s_keys[pos] = key;
+                        }
                     }
                     off += (uint32_t)popc64(mk);
                 }
             }
-        }
+        });
     };
     collect(false);
     __syncthreads();
     const int n = (int)s_ctr[0];
+#if NSG_SCAN_DIAG == 2  // passes 1 and 2 only
+    if (tid == 0) count[b] = 0u;
+    return;
+#endif
     if (n <= FAST_NL) {
         if (tid == 0) count[b] = (unsigned int)n;
         fast_tail<T, DECODE>(p, w, b, n, s_keys, keys_out, cap, todo, s_keys, s_aux);
