@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
+    ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
@@ -87,6 +88,58 @@ def cpu_baseline(args, seconds, streams_per_core=16):
             "sample": f"oracle/nsg_oracle.c or_encode_batch: {cores} worker processes (1 core each) x "
                       f"{streams_per_core} streams of 3N(0,1) fp32 rows, V {args.vocab}, topk {args.topk}, "
                       f"{args.payload_bytes}-byte payloads, {dt:.1f} s"}
+
+
+def wide_path(args, rank, world, dev, steps=10, warmup=3):
+    """The api default quality (precision 16, topk 50,000: api.py:81-86) at the coder batch: the wide path
+    (csrc/nsg_wide.hip) on resident 3*N(0,1) fp32 logits, 1-KiB payloads, whole steps timed with HIP events on
+    the launch stream.  A side line: the headline is the code_base C3 configuration above."""
+    import torch
+    import torch.distributed as dist
+
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.coder import CoderContext, CoderParams, EncodeSession, row_stride
+    from neuralsteganography_amd.dist import reduce_job, shard_range
+
+    V, B = args.vocab, args.batch
+    params = CoderParams(vocab=V, precision=16, temp=1.0, topk=50000, dtype="f32")
+    ctx = CoderContext(params, max_batch=B)
+    ld = row_stride(V, "f32")
+    g = torch.Generator(device=dev)
+    pool = []
+    for i in range(3):
+        g.manual_seed(1000 * rank + i)
+        pool.append(3.0 * torch.randn((B, ld), generator=g, device=dev))
+    mine = shard_range(B * world, world, rank)
+    sess = EncodeSession(ctx, [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.payload_bytes))
+                               for s in mine])
+    for t in range(warmup):
+        sess.step(pool[t % 3])
+    bp0 = sess.fields()["bit_pos"].astype("int64").sum()
+    nt0 = sess.fields()["ntokens"].astype("int64").sum()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for t in range(steps):
+        sess.step(pool[t % 3])
+    end.record()
+    torch.cuda.synchronize()
+    elapsed = start.elapsed_time(end) / 1e3
+    sess.raise_errors()
+    f = sess.fields()
+    nbits = int(f["bit_pos"].astype("int64").sum() - bp0)
+    ntok = int(f["ntokens"].astype("int64").sum() - nt0)
+    bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
+    alg = B * (V * 4 + 76)  # the row read once + state/token/payload window, per step
+    del pool, sess, ctx
+    torch.cuda.empty_cache()
+    return {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
+            "ms_per_step": 1e3 * el_max / steps, "steps": steps,
+            "achieved_gbs": alg / (el_max / steps) / 1e9, "peak_gbs": HBM_PEAK_GBS,
+            "workload": f"api default quality: {B} streams/GPU x ns_encode_step, precision 16, topk 50000, temp 1.0, "
+                        f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
 def end_to_end(args, rank, world, dev):
@@ -268,6 +321,8 @@ def main():
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     del pool, sess, ctx
     torch.cuda.empty_cache()
+    if not args.no_wide:
+        out["wide_path"] = wide_path(args, rank, world, dev)
     if not args.no_e2e:
         out["end_to_end"] = end_to_end(args, rank, world, dev)
     if want_cpu:
