@@ -1,16 +1,21 @@
 // nsg_wide.hip -- the coder step for top-k beyond the single-pass kernel's LDS candidate buffer
 // (e.g. the api default topk 50,000 at precision 16, or the message->bits mode, precision 40 / topk 60,000,
-// code_base/run_single.py:52-54).  Same canonical arithmetic as the single-pass kernel and the oracle.
+// code_base/run_single.py:52-54), and the src rank coder.  Same canonical arithmetic as the single-pass kernel
+// and the oracle.
 //
-//   1. wide_stats_kernel   (wave per stream)  : one streaming pass -> row max, second max, fast-sum interval
-//   2. wide_collect_kernel (blocks per chunk) : every id that can clear the 1/R cutoff, plus the top two,
-//                                               written as 49-bit (value desc, id asc) keys to a segment
-//   3. wide_fast_kernel    (512 threads/stream): streams with <= 8,192 keys: LDS sort + the canonical tail
-//   4. rocprim::segmented_radix_sort_keys_desc : descending sort of the larger streams' keys
-//   5. wide_cdf_kernel     (1024 threads/stream): the other streams: cutoff, canonical sums, rint, int64 scan,
-//                                               overfill, selection, interval update
-// An id left out by step 2 has e_i < S_lo/R <= S/R, i.e. p_i < 1/R for certain, so the first rank below the
-// cutoff lies inside the collected prefix or right after it.
+// Coder step (ns_encode_step / ns_decode_step / ns_sample_step with K > the single-pass limit):
+//   1. wide_scan_kernel    (512 threads/stream): pass 1 over the row -> max, second max, fast-sum interval;
+//                          pass 2 -> every id that can clear the 1/R cutoff, plus the top two, as 49-bit
+//                          (value desc, id asc) keys in LDS; <= 8,192 keys: LDS sort + the canonical tail
+//                          (fast_tail).  Other streams: keys to global memory, stream id onto a work list.
+//   2. rocprim::segmented_radix_sort_keys_desc : descending sort of the listed streams' keys (> 8,192 keys)
+//   3. wide_cdf_kernel     (1024 threads/block, over the work list): cutoff, canonical sums (the exact row sum
+//                          when the fast-sum interval is ambiguous), rint, int64 scan, overfill, selection,
+//                          interval update
+// Rank coder (ns_rank_*_step): wide_stats_kernel (wave per stream) -> wide_collect_kernel (blocks per chunk,
+// every valid id) -> the device-wide sort -> wide_rank_kernel.
+// An id left out of the collection has e_i < S_lo/R <= S/R, i.e. p_i < 1/R for certain, so the first rank
+// below the cutoff lies inside the collected prefix or right after it.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
