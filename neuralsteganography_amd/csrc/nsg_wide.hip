@@ -704,6 +704,9 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 #ifndef NSG_SCAN_DIAG
 #define NSG_SCAN_DIAG 0
 #endif
+#ifndef NSG_SCAN_VEC_BYTES
+#define NSG_SCAN_VEC_BYTES 64  // row bytes per thread per group in the two sweeps (two groups in flight)
+#endif
 #ifndef NSG_SCAN_P1_KEEP
 #define NSG_SCAN_P1_KEEP 1  // pass 1 loads with the default policy (0: non-temporal, for A/B timing)
 #endif
@@ -1097,7 +1100,7 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
     __shared__ uint64_t s_keys[FAST_NL];
     __shared__ uint64_t s_aux[FAST_NB / 2];
     constexpr int W = Elem<T>::W;
-    constexpr int G = 16 / W;                 // vectors in flight per thread (64 B)
+    constexpr int G = NSG_SCAN_VEC_BYTES / (4 * W);  // 16-B vectors per thread per block row group
     constexpr int TS = FAST_THREADS * W;      // ids per block-wide vector row
     const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     const ns_stream_state st = p.state[b];
