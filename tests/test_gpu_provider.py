@@ -249,16 +249,19 @@ def test_gpt2_fp16_decode_hip_attention_matches_sdpa_and_hf():
     assert (la[1, :50257].float().cpu() - ref).abs().max().item() < 3e-2
 
 
-@pytest.mark.parametrize("cap_extra", [None, 12])
-def test_graph_captured_encode_matches_eager(cap_extra):
+@pytest.mark.parametrize("cap_extra,topk", [(None, 300), (12, 300), (None, 50000)])
+def test_graph_captured_encode_matches_eager(cap_extra, topk):
     """encode_batch with the per-token step captured as a hipGraph (coder + GPT-2 decode, cache length on the
     device) gives the same tokens as the eager loop, including when the preallocated cache runs out and the
-    loop continues eagerly (cap_extra: cache limited to context + 12 positions)."""
+    loop continues eagerly (cap_extra: cache limited to context + 12 positions), and for the api default
+    quality (precision 16, topk 50,000), whose wide-path launches (memset, fused scan, device-wide sort,
+    list kernel) are captured too."""
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
     m = random_gpt2("gpt2", seed=31)
-    q = {"temp": 0.9, "precision": 26, "topk": 300}
+    q = {"temp": 0.9, "precision": 26, "topk": 300} if topk == 300 else {"temp": 1.0, "precision": 16,
+                                                                        "topk": topk}
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 12)) for s in range(3)]
     ctx = synthetic.DEFAULT_CONTEXT
     out = {}
