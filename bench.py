@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
     ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-logits (PCIe-inclusive) side figure")
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
@@ -191,6 +192,31 @@ def end_to_end(args, rank, world, dev):
     return out
 
 
+def host_logits_rate(args, sess, logits, stream, steps=5):
+    """PCIe-inclusive side figure (never `value`): the same coder step when the caller hands over the logit
+    batch in pinned host memory, i.e. one H2D copy of [B, ld] per step before ns_encode_step (this GPU only)."""
+    import torch
+
+    host = logits.cpu().pin_memory()
+    dev_buf = torch.empty_like(logits)
+    f0 = sess.fields()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    start.record(stream)
+    for _ in range(steps):
+        dev_buf.copy_(host, non_blocking=True)
+        sess.step(dev_buf)
+    end.record(stream)
+    torch.cuda.synchronize()
+    sec = start.elapsed_time(end) / 1e3 / steps
+    bits = int(sess.fields()["bit_pos"].sum() - f0["bit_pos"].sum())
+    nbytes = host.numel() * host.element_size()
+    del host, dev_buf
+    return {"ms_per_step": sec * 1e3, "value": bits / steps / sec, "unit": "payload bits/s",
+            "h2d_bytes_per_step": nbytes, "h2d_gbs": nbytes / sec / 1e9,
+            "note": "logits copied from pinned host memory each step, this GPU only; not the headline"}
+
+
 def measured_traffic(args, version):
     """Per-launch HBM bytes from a committed rocprofv3 PMC record (tools/pmc_traffic.py) of THIS library
     build and workload, else None."""
@@ -273,6 +299,7 @@ def main():
     spec_misses = c1[2] - c0[2]
     bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
     sess.raise_errors()
+    pcie = None if args.no_pcie else host_logits_rate(args, sess, pool[0], stream)
 
     bits_all, ss_all, elapsed_max, kern_ms_max = reduce_job(bits, stream_steps, elapsed, kern_ms, device=dev)
 
@@ -318,6 +345,8 @@ def main():
                      "traffic_source": traffic[1] if traffic else None,
                      "kernel": f"coder_step_kernel<{'_Float16' if args.dtype == 'f16' else 'float'},false>", "alg_bytes_per_launch": alg_bytes},
     }
+    if pcie is not None:
+        out["host_logits_pcie"] = pcie
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     del pool, sess, ctx
     torch.cuda.empty_cache()

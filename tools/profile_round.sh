@@ -15,11 +15,11 @@ ver=$(python -c 'from neuralsteganography_amd import _lib; print(_lib.version())
 echo "library: $ver" > "$out/version.txt"
 timeout -k 10 300 python bench.py "$@" > "$out/bench.json" 2> "$out/bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- \
-    python bench.py --no-cpu-baseline --no-e2e --no-wide "$@" > "$out/trace.log" 2>&1
+    python bench.py --no-cpu-baseline --no-e2e --no-wide --no-pcie "$@" > "$out/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fetch" -o run --output-format csv -- \
-    python bench.py --no-cpu-baseline --no-e2e --no-wide --steps 20 --warmup 2 "$@" > "$out/pmc_fetch.log" 2>&1
+    python bench.py --no-cpu-baseline --no-e2e --no-wide --no-pcie --steps 20 --warmup 2 "$@" > "$out/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/pmc_write" -o run --output-format csv -- \
-    python bench.py --no-cpu-baseline --no-e2e --no-wide --steps 20 --warmup 2 "$@" > "$out/pmc_write.log" 2>&1
+    python bench.py --no-cpu-baseline --no-e2e --no-wide --no-pcie --steps 20 --warmup 2 "$@" > "$out/pmc_write.log" 2>&1
 fetch=$(find "$out/pmc_fetch" -name '*counter_collection.csv' -print -quit)
 write=$(find "$out/pmc_write" -name '*counter_collection.csv' -print -quit)
 python tools/pmc_traffic.py "$fetch" "$write" "$out/pmc_traffic.json" --version "$ver"
