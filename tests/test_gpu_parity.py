@@ -279,8 +279,9 @@ def test_adversarial_rows_exercise_fallback_paths(mode):
         assert c1[3] > c0[3], "slow top-K selection path was not exercised"
 
 
-@pytest.mark.parametrize("mode", ["plain", "ties", "outlier", "mixed"])
-def test_wide_lds_path_matches_oracle(mode):
+@pytest.mark.parametrize("mode,dtype", [("plain", "f32"), ("ties", "f32"), ("outlier", "f32"), ("mixed", "f32"),
+                                        ("ties", "f16"), ("mixed", "f16")])
+def test_wide_lds_path_matches_oracle(mode, dtype):
     """The wide path's LDS sort (streams with <= 8,192 collected keys, api defaults precision 16 / topk 50,000):
     'plain' rows keep 2-5k keys (counting sort + in-bucket ranks), 'ties' quantises the logits so a few values
     hold thousands of keys each (over-full buckets -> bitonic sort), 'outlier' leaves the top two keys only (every other step),
@@ -290,10 +291,11 @@ def test_wide_lds_path_matches_oracle(mode):
 
     torch = _torch()
     V, B = 50257, 4
-    params = CoderParams(vocab=V, precision=16, temp=1.0, topk=50000)
+    params = CoderParams(vocab=V, precision=16, temp=1.0, topk=50000, dtype=dtype)
     ctx = _ctx(params, B)
     assert ctx.wide
-    ld = row_stride(V, "f32")
+    ld = row_stride(V, dtype)
+    npdt = np.float16 if dtype == "f16" else np.float32
     kinds = {"plain": ["plain"] * B, "ties": ["ties"] * B, "outlier": ["outlier"] * B,
              "mixed": ["plain", "ties", "outlier", "flat"]}[mode]
 
@@ -303,15 +305,15 @@ def test_wide_lds_path_matches_oracle(mode):
         if kind == "ties":
             x = np.round(x * 2.0) / 2.0
         elif kind == "outlier" and t % 2 == 0:  # (every step would carry no bits at all)
-            x[(97 * t + 13 * s) % (V - 2)] = 3.0e30
-        return x.astype(np.float32)
+            x[(97 * t + 13 * s) % (V - 2)] = 6.0e4 if dtype == "f16" else 3.0e30
+        return x.astype(npdt)
 
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 6)) for s in range(B)]
     expect = [oracle.encode_stream(lambda t, s=s: row(s, t), bits[s], banned=params.banned_ids(), temp=1.0,
                                    precision=16, topk=50000)[0] for s in range(B)]
 
     def fn(t, _last=None):
-        arr = np.zeros((B, ld), np.float32)
+        arr = np.zeros((B, ld), npdt)
         for s in range(B):
             arr[s, :V] = row(s, t)
         return torch.from_numpy(arr).cuda()
