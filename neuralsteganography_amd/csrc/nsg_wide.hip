@@ -290,15 +290,31 @@ __device__ __forceinline__ double block_canonical_butterfly(double* sm64) {
 
 template <typename T>
 __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, double m, double* ebuf, double* sm64) {
-    // canonical order: id j -> lane (j>>2)&63, per-lane increasing; exps computed in parallel per round
+    // canonical order: id j -> lane (j>>2)&63, per-lane increasing; exps computed in parallel per round; the
+    // next round's logits are loaded into registers before this round's ordered chain runs (a second LDS
+    // buffer to overlap the chain with the next round's exps measured no faster)
+    constexpr int PT = WIDE_ROUND / WIDE_THREADS;
     double acc = 0.0;
+    float xv[PT];
+    auto load_round = [&](int base) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int j = base + u * WIDE_THREADS + (int)threadIdx.x;
+            xv[u] = j < p.V ? Elem<T>::load1(rowc, j) : 0.0f;
+        }
+    };
+    load_round(0);
     for (int base = 0; base < p.V; base += WIDE_ROUND) {
-        for (int i = threadIdx.x; i < WIDE_ROUND; i += WIDE_THREADS) {
+        double* eb = ebuf;
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int i = u * WIDE_THREADS + (int)threadIdx.x;
             const int j = base + i;
             double e = 0.0;
-            if (j < p.V && !is_banned(p, j)) e = exp_canon(((double)(Elem<T>::load1(rowc, j) + 0.0f) - m) * p.inv_temp);
-            ebuf[i] = e;
+            if (j < p.V && !is_banned(p, j)) e = exp_canon(((double)(xv[u] + 0.0f) - m) * p.inv_temp);
+            eb[i] = e;
         }
+        if (base + WIDE_ROUND < p.V) load_round(base + WIDE_ROUND);
         __syncthreads();
         if (threadIdx.x < 64) {
             // groups of this round in increasing order: g = base/4 + g_local, lane = g & 63; four groups' loads
@@ -310,13 +326,13 @@ __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, dou
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) t[4 * u + q] = ebuf[4 * (gl + 64 * u) + q];
+                    for (int q = 0; q < 4; ++q) t[4 * u + q] = eb[4 * (gl + 64 * u) + q];
 #pragma unroll
                 for (int v = 0; v < 16; ++v) acc += t[v];
             }
             for (; gl < WIDE_ROUND / 4; gl += 64) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc += ebuf[4 * gl + q];
+                for (int q = 0; q < 4; ++q) acc += eb[4 * gl + q];
             }
         }
         __syncthreads();
@@ -731,9 +747,9 @@ __device__ __forceinline__ int wave_min_int(int v) {
 // the LDS path for one stream whose n <= FAST_NL collected keys sit at `kin` (global or LDS, any order): sort,
 // then the canonical tail; every thread of the 512-thread block calls it
 template <typename T, bool DECODE>
-__device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w, const int b, const int n,
-                                          const uint64_t* kin, uint64_t* keys_out, const int cap, unsigned int* todo,
-                                          uint64_t* s_keys, uint64_t* s_aux) {
+__device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w, WideStat* wsb, const int b,
+                                          const int n, const uint64_t* kin, uint64_t* keys_out, const int cap,
+                                          unsigned int* todo, uint64_t* s_keys, uint64_t* s_aux) {
     uint32_t* s_cnt = (uint32_t*)s_aux;
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     // ---- load (unsorted, as collected) + key range
@@ -931,6 +947,9 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     // ambiguous cutoff (the exact row sum: measured cheaper in the list kernel than in this one, whose
     // workgroup slots are the row stream's) or a degenerate row: wide_cdf_kernel
     if (fa < fb || k > Kc) {
+        // an ambiguous cutoff is marked exact, so wide_cdf_kernel goes straight to the exact row sum (it would
+        // find the same ambiguity first)
+        if (fa < fb && tid == 0) wsb->exact = 1u;
         defer();
         return;
     }
@@ -1338,7 +1357,7 @@ __global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p
 #endif
     if (n <= FAST_NL) {
         if (tid == 0) count[b] = (unsigned int)n;
-        fast_tail<T, DECODE>(p, w, b, n, s_keys, keys_out, cap, todo, s_keys, s_aux);
+        fast_tail<T, DECODE>(p, w, &ws[b], b, n, s_keys, keys_out, cap, todo, s_keys, s_aux);
         return;
     }
     __syncthreads();
