@@ -6,9 +6,9 @@
 // Coder step (ns_encode_step / ns_decode_step / ns_sample_step with K > the single-pass limit):
 //   1. wide_scan_kernel    (512 threads/stream): pass 1 over the row -> max, second max, fast-sum interval;
 //                          pass 2 -> every id that can clear the 1/R cutoff, plus the top two, as 49-bit
-//                          (value desc, id asc) keys in LDS; <= 8,192 keys: LDS sort + the canonical tail
+//                          (value desc, id asc) keys in LDS; <= 5,632 keys: LDS sort + the canonical tail
 //                          (fast_tail).  Other streams: keys to global memory, stream id onto a work list.
-//   2. rocprim::segmented_radix_sort_keys_desc : descending sort of the listed streams' keys (> 8,192 keys)
+//   2. rocprim::segmented_radix_sort_keys_desc : descending sort of the listed streams' keys (> 5,632 keys)
 //   3. wide_cdf_kernel     (1024 threads/block, over the work list): cutoff, canonical sums (the exact row sum
 //                          when the fast-sum interval is ambiguous), rint, int64 scan, overfill, selection,
 //                          interval update
@@ -716,7 +716,9 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 // canonical tail on the sorted keys: the same arithmetic, in the same order, as wide_cdf_kernel.  Streams that
 // need the exact row sum, the row-statistics fallback, the sampler, or hit an error are handed to
 // wide_cdf_kernel (listed in todo) with their sorted keys written to keys_out; streams with more keys were
-// sorted by the device-wide sort and are listed too.  80,896 B of LDS: two workgroups per CU.
+// sorted by the device-wide sort and are listed too.  53,248 B of LDS and <= 80 VGPRs: three workgroups per
+// CU (measured 0.53 vs 0.58 ms per step with 8,192 keys / 3,840 buckets at two per CU: more rows in flight while
+// other workgroups run their latency-bound tails).
 #ifndef NSG_SCAN_DIAG
 #define NSG_SCAN_DIAG 0
 #endif
@@ -728,9 +730,18 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 #endif
 constexpr int FAST_THREADS = 512;
 constexpr int FAST_WAVES = FAST_THREADS / WAVE;
-constexpr int FAST_NL = 8192;                      // keys of a stream sorted in LDS
+#ifndef NSG_FAST_NL
+#define NSG_FAST_NL 5632
+#endif
+#ifndef NSG_FAST_NB
+#define NSG_FAST_NB 2048
+#endif
+#ifndef NSG_FAST_WAVES_PER_SIMD
+#define NSG_FAST_WAVES_PER_SIMD 6  // launch-bounds occupancy target: 6 = three 512-thread workgroups per CU
+#endif
+constexpr int FAST_NL = NSG_FAST_NL;               // keys of a stream sorted in LDS
 constexpr int FAST_R = FAST_NL / FAST_THREADS;     // ranks per thread: rank i = r * FAST_THREADS + tid
-constexpr int FAST_NB = 3840;                      // counting-sort buckets over [kmin, kmax]
+constexpr int FAST_NB = NSG_FAST_NB;               // counting-sort buckets over [kmin, kmax]
 constexpr uint32_t FAST_OCC_MAX = 48;              // fuller bucket -> bitonic sort
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int off) {
@@ -838,8 +849,6 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         const int i = r * FAST_THREADS + tid;
         if (i < n) s_keys[s_cnt[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = kr[r];
     }
-    if (bitonic)
-        for (int i = n + tid; i < P2; i += FAST_THREADS) s_keys[i] = 0ull;  // below every real key
     __syncthreads();
     if (!bitonic) {
         // rank = bucket start + larger keys in the bucket (keys are distinct: ids are)
@@ -862,18 +871,38 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         }
         __syncthreads();
     } else {
-        for (int size = 2; size <= P2; size <<= 1)
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                for (int t = tid; t < P2 / 2; t += FAST_THREADS) {
-                    const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        // bitonic network in its one-direction form (every compare-exchange puts the larger key at the lower
+        // index: a mirror stage, then half-cleaners), over P2 = next power of two >= n positions of which only
+        // [0, n) exist: a pair whose upper index is >= n pairs a real key with a virtual minimum, already in
+        // order, so it is skipped and nothing is stored beyond n (P2 may exceed the LDS array)
+        for (int size = 2; size <= P2; size <<= 1) {
+            const int half = size >> 1;
+            for (int t = tid; t < P2 / 2; t += FAST_THREADS) {
+                const int base = (t / half) * size, off = t % half;
+                const int i = base + off, j = base + size - 1 - off;
+                if (j < n) {
                     const uint64_t a = s_keys[i], c = s_keys[j];
-                    if ((a < c) == ((i & size) == 0)) {
+                    if (a < c) {
                         s_keys[i] = c;
                         s_keys[j] = a;
                     }
                 }
+            }
+            __syncthreads();
+            for (int stride = half >> 1; stride > 0; stride >>= 1) {
+                for (int t = tid; t < P2 / 2; t += FAST_THREADS) {
+                    const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+                    if (j < n) {
+                        const uint64_t a = s_keys[i], c = s_keys[j];
+                        if (a < c) {
+                            s_keys[i] = c;
+                            s_keys[j] = a;
+                        }
+                    }
+                }
                 __syncthreads();
             }
+        }
     }
     // ---- sorted keys of this thread's ranks into registers; s_keys becomes the e_i array
     uint64_t ks[FAST_R];
@@ -1098,7 +1127,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
 // One 512-thread workgroup per stream does passes 1 and 2 and, for the usual stream, the whole step:
 //   pass 1: stream the row once (default cache policy) -> max, second max, the proven fast-sum interval
 //           (fp32 groups of W terms, as wide_stats_kernel: the same bound)
-//   pass 2: stream it again -- two workgroups per CU keep ~512 rows (~100 MB fp32) in flight, within the
+//   pass 2: stream it again -- three workgroups per CU keep ~768 rows (~155 MB fp32) in flight, within the
 //           256 MiB Infinity Cache, so the re-read can be served there (a non-temporal pass 1 measured 4 % slower
 //           overall) -- collecting the ids that can clear the cutoff into LDS
 //   then fast_tail (LDS sort + canonical tail).  More than FAST_NL keys: pass 3 writes them to keys_in for the
@@ -1114,7 +1143,7 @@ __device__ __forceinline__ double uni_f64(double v) {
 }
 
 template <typename T, bool DECODE>
-__global__ __launch_bounds__(FAST_THREADS, 4) void wide_scan_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+__global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_scan_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
                                                                    uint64_t* keys_out, unsigned int* count, int cap,
                                                                    unsigned int* todo) {
     __shared__ uint64_t s_keys[FAST_NL];
