@@ -326,3 +326,36 @@ def test_wide_lds_path_matches_oracle(mode, dtype):
     got = decode_batch(ctx, toks, fn)
     for s in range(B):
         assert got[s][: len(bits[s])] == bits[s]
+
+
+def test_wide_list_kernel_grid_stride_over_many_streams():
+    """More streams handed to the list kernel than it has workgroups (256): every step forces the exact row sum
+    (so every stream is listed), and half the rows are flat enough to overflow
+    the LDS path (device-wide sort).  Tokens must match the oracle for every stream."""
+    from neuralsteganography_amd.coder import CoderParams, decode_batch, encode_batch, row_stride
+
+    V, B = 50257, 258
+    params = CoderParams(vocab=V, precision=16, temp=1.0, topk=50000)
+    ctx = _ctx(params, B)
+    ld = row_stride(V, "f32")
+    seed = 23
+    scales = [0.5 if s % 2 else 3.0 for s in range(B)]
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 2)) for s in range(B)]
+    expect = [oracle.encode_stream(lambda t, s=s: synthetic.logits_row(seed, s, t, V, scales[s]), bits[s],
+                                   banned=params.banned_ids(), temp=1.0, precision=16, topk=50000)[0]
+              for s in range(B)]
+    torch = _torch()
+
+    def fn(t, _last=None):
+        arr = np.zeros((B, ld), np.float32)
+        for s in range(B):
+            arr[s, :V] = synthetic.logits_row(seed, s, t, V, scales[s])
+        return torch.from_numpy(arr).cuda()
+
+    c0 = ctx.counters()
+    toks = encode_batch(ctx, bits, fn, force_exact=True)
+    assert toks == expect
+    assert ctx.counters()[0] - c0[0] >= B, "the exact-sum path did not run for every stream"
+    got = decode_batch(ctx, toks, fn)
+    for s in range(B):
+        assert got[s][: len(bits[s])] == bits[s]
