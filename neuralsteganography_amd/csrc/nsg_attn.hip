@@ -3,7 +3,8 @@
 // Reference semantics: Hugging Face GPT2Attention for one new token per stream over the unbounded cache the
 // reference keeps (code_base/arithmetic.py:115-122): softmax(q k^T / sqrt(D)) v over positions 0..L0.
 //
-// Layout: one wavefront per (stream, head).  Lane l holds dims 8*(l&7)..+7 of key row (l>>3) of an 8-row
+// Layout: one wavefront per (stream, head) -- or, for small batches, a workgroup of 4 or 8 waves per pair that
+// split the rows and merge their partials through LDS (decode_attn_kernel<NSPLIT>).  Lane l holds dims 8*(l&7)..+7 of key row (l>>3) of an 8-row
 // chunk, so an 8-lane group reads one 128-byte K (and V) row and the wave reads 1 KiB of contiguous cache per
 // 16-byte load instruction.  Scores are reduced inside the 8-lane group; each group keeps its own online
 // softmax (running max, sum, 8 accumulator dims) over the rows it saw, and the 8 groups are merged once at the
@@ -40,17 +41,21 @@ __device__ __forceinline__ void unpack8(f16x8 v, float* f) {
     for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
 }
 
-__global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Float16* __restrict__ qkv,
-                                                                     int64_t qkv_stride, _Float16* kc, _Float16* vc,
-                                                                     int64_t cb, int64_t ch, int B, int H, int L0,
-                                                                     const int32_t* __restrict__ L0p, int cap,
-                                                                     _Float16* __restrict__ out, int64_t out_stride,
-                                                                     float scale_log2) {
+// NSPLIT = 1: one wave per (stream, head), ATT_WAVES pairs per workgroup (large batches: enough waves).
+// NSPLIT > 1: one workgroup of NSPLIT waves per pair (small batches: a lone wave per pair leaves the chip
+// idle); wave w takes the 32-row chunks w, w + NSPLIT, ... and the NSPLIT online-softmax partials are merged
+// through LDS by wave 0 -- no cross-workgroup hand-off.
+template <int NSPLIT>
+__global__ __launch_bounds__(64 * (NSPLIT > 1 ? NSPLIT : ATT_WAVES)) void decode_attn_kernel(
+    const _Float16* __restrict__ qkv, int64_t qkv_stride, _Float16* kc, _Float16* vc, int64_t cb, int64_t ch, int B,
+    int H, int L0, const int32_t* __restrict__ L0p, int cap, _Float16* __restrict__ out, int64_t out_stride,
+    float scale_log2) {
     if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
     if (L0 < 0 || L0 >= cap) return;                     // never write past the cache (host checks capacity)
     const int lane = threadIdx.x & 63;
-    const int pair = blockIdx.x * ATT_WAVES + (threadIdx.x >> 6);
-    if (pair >= B * H) return;
+    const int wv = NSPLIT > 1 ? (int)(threadIdx.x >> 6) : 0;  // split index
+    const int pair = NSPLIT > 1 ? (int)blockIdx.x : (int)(blockIdx.x * ATT_WAVES + (threadIdx.x >> 6));
+    if (pair >= B * H) return;  // (NSPLIT > 1: uniform over the workgroup, before any barrier)
     const int b = pair / H;
     const int h = pair - b * H;
     const int g = lane >> 3;  // row within an 8-row chunk
@@ -62,7 +67,7 @@ __global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Floa
     const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
     _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
     _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
-    if (g == 0) {  // KV append of the new token (position L0)
+    if (g == 0 && wv == 0) {  // KV append of the new token (position L0)
         *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
         *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
     }
@@ -73,7 +78,7 @@ __global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Floa
 #pragma unroll
     for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
 
-    for (int j0 = 0; j0 < Lk; j0 += 8 * ATT_U) {
+    for (int j0 = wv * 8 * ATT_U; j0 < Lk; j0 += NSPLIT * 8 * ATT_U) {
         f16x8 kr[ATT_U], vr[ATT_U];
 #pragma unroll
         for (int u = 0; u < ATT_U; ++u) {
@@ -129,6 +134,34 @@ __global__ __launch_bounds__(64 * ATT_WAVES) void decode_attn_kernel(const _Floa
         }
         m = mn;
     }
+    if constexpr (NSPLIT > 1) {
+        // every lane now holds its wave's merged (m, l) and the 8 dims of slice c: waves 1.. hand theirs to wave 0
+        __shared__ float s_m[NSPLIT], s_l[NSPLIT];
+        __shared__ float s_acc[NSPLIT][ATT_D];
+        if (g == 0) {
+#pragma unroll
+            for (int d = 0; d < 8; ++d) s_acc[wv][c * 8 + d] = acc[d];
+            if (c == 0) {
+                s_m[wv] = m;
+                s_l[wv] = l;
+            }
+        }
+        __syncthreads();
+        if (wv != 0) return;
+        float mt = s_m[0];
+#pragma unroll
+        for (int w = 1; w < NSPLIT; ++w) mt = fmaxf(mt, s_m[w]);
+        l = 0.0f;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NSPLIT; ++w) {
+            const float f = exp2f(s_m[w] - mt);
+            l += s_l[w] * f;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) acc[d] += s_acc[w][c * 8 + d] * f;
+        }
+    }
     if (g == 0) {
         const float inv = 1.0f / l;
         f16x8 w;
@@ -156,10 +189,20 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
     const float scale_log2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(nsg::decode_attn_kernel, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
-                       dim3(64 * nsg::ATT_WAVES), 0, (hipStream_t)hip_stream, (const _Float16*)d_qkv, qkv_stride,
-                       (_Float16*)d_k_cache, (_Float16*)d_v_cache, cache_b_stride, cache_h_stride, B, H, L0, d_L0,
-                       cap, (_Float16*)d_out, out_stride, scale_log2);
+    // waves per pair by batch size: a launch wants well over the chip's 256 CUs x a few waves
+    const hipStream_t st = (hipStream_t)hip_stream;
+    const _Float16* q = (const _Float16*)d_qkv;
+    _Float16 *k = (_Float16*)d_k_cache, *v = (_Float16*)d_v_cache, *o = (_Float16*)d_out;
+    if (pairs <= 256)
+        hipLaunchKernelGGL(nsg::decode_attn_kernel<8>, dim3(pairs), dim3(64 * 8), 0, st, q, qkv_stride, k, v,
+                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
+    else if (pairs <= 1024)
+        hipLaunchKernelGGL(nsg::decode_attn_kernel<4>, dim3(pairs), dim3(64 * 4), 0, st, q, qkv_stride, k, v,
+                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
+    else
+        hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
+                           dim3(64 * nsg::ATT_WAVES), 0, st, q, qkv_stride, k, v, cache_b_stride, cache_h_stride, B,
+                           H, L0, d_L0, cap, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 

@@ -182,7 +182,9 @@ def test_batched_front_end_multi_message_roundtrip():
 
 
 @pytest.mark.parametrize("B,H,L0", [(3, 12, 0), (3, 12, 1), (5, 12, 7), (4, 16, 8), (2, 12, 33), (7, 12, 200),
-                                    (2, 16, 1023)])
+                                    (2, 16, 1023), (1, 12, 500),  # <= 256 pairs: 8 waves per pair
+                                    (40, 12, 77), (64, 16, 3),    # <= 1024 pairs: 4 waves per pair
+                                    (100, 12, 50)])               # one wave per pair
 def test_hip_decode_attention_matches_fp32_reference(B, H, L0):
     """ns_decode_attention (csrc/nsg_attn.hip) vs softmax(q k^T / sqrt(D)) v in fp32 (torch) over the cache
     plus the appended token; the kernel must also have written the new k/v at position L0.  fp16 output:
