@@ -137,6 +137,9 @@ class CoderContext:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            torch = _torch()
+            if torch.cuda.is_available():  # launches still queued may read the context's buffers
+                torch.cuda.synchronize(self.device)
             _lib.lib().ns_destroy(self._h)
             self._h = None
 
@@ -145,6 +148,19 @@ class CoderContext:
             self.close()
         except Exception:
             pass
+
+
+def _check_logits(ctx: "CoderContext", B: int, logits) -> None:
+    """Host-side validation before any launch that reads a logit matrix: dtype of the context, [B, ld] with
+    unit column stride, ld >= vocab, on this context's device (a mismatch would make the kernel misread rows
+    or read past their end)."""
+    p = ctx.params
+    if logits.dtype != p.torch_dtype or logits.dim() != 2 or logits.shape[0] != B:
+        raise ConfigurationError(f"logits must be [{B}, ld] {p.dtype}")
+    if logits.stride(1) != 1 or logits.shape[1] < p.vocab or logits.stride(0) < p.vocab or not logits.is_cuda:
+        raise ConfigurationError("logits must be contiguous rows on the GPU with ld >= vocab")
+    if logits.device.index != ctx.device:
+        raise ConfigurationError(f"logits on cuda:{logits.device.index}, coder context on cuda:{ctx.device}")
 
 
 def _state_tensor(B: int, device):
@@ -244,11 +260,7 @@ class EncodeSession:
         return self.out_token
 
     def _check_logits(self, logits) -> None:
-        p = self.ctx.params
-        if logits.dtype != p.torch_dtype or logits.dim() != 2 or logits.shape[0] != self.B:
-            raise ConfigurationError(f"logits must be [{self.B}, ld] {p.dtype}")
-        if logits.stride(1) != 1 or logits.shape[1] < p.vocab or not logits.is_cuda:
-            raise ConfigurationError("logits must be contiguous rows on the GPU with ld >= vocab")
+        _check_logits(self.ctx, self.B, logits)
 
     def all_done(self) -> bool:
         return bool(np.all(_state_fields(self.state)["flags"] & _lib.NS_ST_DONE))
@@ -338,6 +350,7 @@ class DecodeSession:
         if self.t >= self.T:
             raise ConfigurationError("all tokens already decoded")
         t = self.t
+        _check_logits(self.ctx, self.B, logits)
         flags = _lib.NS_STEP_FORCE_EXACT_SUM if force_exact else 0
         rc = _lib.lib().ns_decode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok[t]), _ptr(self.last[t]),
@@ -351,6 +364,7 @@ class DecodeSession:
         gathered into fixed buffers by the device, so one captured hipGraph serves every step.  Returns the
         token buffer (the LM's next input)."""
         torch = _torch()
+        _check_logits(self.ctx, self.B, logits)
         if getattr(self, "d_t", None) is None:
             self.d_t = torch.full((1,), self.t, dtype=torch.long, device=self.state.device)
             self.tok_s = torch.empty((1, self.B), dtype=self.tok.dtype, device=self.state.device)
@@ -444,9 +458,7 @@ class SampleSession:
         return self.trace
 
     def step(self, logits, *, diag_flags: int = 0):
-        p = self.ctx.params
-        if logits.dtype != p.torch_dtype or logits.dim() != 2 or logits.shape[0] != self.B or not logits.is_cuda:
-            raise ConfigurationError(f"logits must be [{self.B}, ld] {p.dtype} on the GPU")
+        _check_logits(self.ctx, self.B, logits)
         if self.steps >= self.hist.shape[1]:
             raise ConfigurationError("token history full: raise max_tokens")
         rc = _lib.lib().ns_sample_step(
@@ -518,6 +530,7 @@ class StreamingDecodeSession:
     def step(self, logits, tokens: Sequence[int], is_last: Sequence[bool], active: Sequence[bool]) -> None:
         torch = _torch()
         p = self.ctx.params
+        _check_logits(self.ctx, self.B, logits)
         f = _state_fields(self.state)
         self._grow(int(f["bit_pos"].max(initial=0)) + 2 * p.precision)
         tok = torch.tensor(np.asarray(tokens, dtype=np.int32), device=self.dev)
@@ -618,6 +631,7 @@ class RankEncodeSession:
         self.cons = torch.zeros((self.B, cap), dtype=torch.int32, device=dev)
 
     def step(self, logits):
+        _check_logits(self.ctx, self.B, logits)
         rc = _lib.lib().ns_rank_encode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
             _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), _ptr(self.cons),
@@ -683,6 +697,7 @@ class RankDecodeSession:
 
     def step(self, logits) -> None:
         t = self.t
+        _check_logits(self.ctx, self.B, logits)
         rc = _lib.lib().ns_rank_decode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok[t]), _ptr(self.keep[t]),
             _ptr(self.act[t]), _ptr(self.state), _ptr(self.out_bits), self.out_stride, self.temp,

@@ -74,6 +74,7 @@ class ByteTokenizer:
         return bytes(int(i) % 256 for i in ids).decode("utf-8", errors="ignore")
 
 
+CTX_CACHE_SIZE = 4  # live coder contexts per provider (distinct quality settings)
 GRAPH_MAX_BATCH = 1024  # auto mode: capture the token step as a hipGraph up to this batch
 
 
@@ -106,6 +107,48 @@ class _StepGraph:
     def replay(self) -> None:
         self.graph.replay()
         self.lm.L += 1
+
+
+class _StopCheck:
+    """The reference's per-token stop test ``stop_text in enc.decode(output)`` (``code_base/arithmetic.py:
+    207-210``) without a host round trip per token.  A new occurrence of ``stop_text`` must end inside the newest
+    token, so that token's text contains the last character of ``stop_text``; a per-id device table of such
+    tokens is gathered by the emitted tokens inside the step (graph-capturable), and the host reads one flag
+    per step and decodes 16-token tails only for the flagged streams."""
+
+    def __init__(self, provider, sess, stop_text: str):
+        import torch
+
+        self.sess, self.stop_text, self.tok = sess, stop_text, provider.tokenizer
+        self.table = provider.stop_table(stop_text)
+        self.hit = torch.zeros(sess.B, dtype=torch.bool, device=sess.state.device)
+        self.any = torch.zeros(1, dtype=torch.bool, device=sess.state.device)
+        self.any_host = torch.zeros(1, dtype=torch.bool).pin_memory()
+
+    def flag(self, tok) -> None:
+        import torch
+
+        live = (self.sess.state.view(torch.int32)[:, 7] & 1) == 0
+        torch.logical_and(self.table.index_select(0, tok.long()), live, out=self.hit)
+        torch.any(self.hit, dim=0, keepdim=True, out=self.any)
+
+    def check(self) -> None:
+        import torch
+
+        self.any_host.copy_(self.any, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        if not bool(self.any_host[0]):
+            return
+        cand = torch.nonzero(self.hit).flatten().cpu().tolist()
+        n = self.sess.fields()["ntokens"]
+        stop = []
+        for i in cand:
+            k = int(n[i])
+            tail = self.sess.hist[i, max(0, k - 16):k].cpu().tolist()
+            if self.stop_text in self.tok.decode(tail):
+                stop.append(i)
+        if stop:
+            self.sess.mark_done(stop)
 
 
 class HipArithmeticLM:
@@ -159,12 +202,22 @@ class HipArithmeticLM:
 
     # ---------------------------------------------------------------- plumbing
     def _coder(self, params: CoderParams, B: int) -> CoderContext:
+        """Coder context for ``params`` serving batches up to ``B``.  Keyed on the parameters only (the kernels
+        take B per call): a context built for a larger batch serves every smaller one, a larger B replaces it,
+        and at most ``CTX_CACHE_SIZE`` parameter sets stay alive (least recently used closed first) -- each
+        wide-path context holds 2*B*V*8 bytes of sort keys."""
         key = (params.vocab, params.precision, params.temp, params.topk, params.dtype,
-               tuple(params.banned_ids()), B)
-        ctx = self._ctx_cache.get(key)
+               tuple(params.banned_ids()))
+        ctx = self._ctx_cache.pop(key, None)
+        if ctx is not None and ctx.max_batch < B:
+            ctx.close()
+            ctx = None
         if ctx is None:
             ctx = CoderContext(params, max_batch=max(B, 1), device=self.device.index)
-            self._ctx_cache[key] = ctx
+        self._ctx_cache[key] = ctx  # re-inserted last: dict order is the LRU order
+        while len(self._ctx_cache) > CTX_CACHE_SIZE:
+            old = next(iter(self._ctx_cache))
+            self._ctx_cache.pop(old).close()
         return ctx
 
     def sentence_end_table(self):
@@ -183,6 +236,26 @@ class HipArithmeticLM:
                     tab[i] = 1
             self._sent_end = tab
         return self._sent_end
+
+    def stop_table(self, stop_text: str):
+        """Device bool table [vocab]: the id's decoded text contains the last character of ``stop_text``
+        (only such a token can complete a new occurrence).  Cached per stop text."""
+        import torch
+
+        cache = self.__dict__.setdefault("_stop_tables", {})
+        tab = cache.get(stop_text)
+        if tab is None:
+            if not stop_text:
+                raise ConfigurationError("stop_text must be non-empty")
+            last = stop_text[-1]
+            host = torch.zeros(self.vocab, dtype=torch.bool)
+            for i in range(self.vocab):
+                try:
+                    host[i] = last in self.tokenizer.decode([i])
+                except Exception:
+                    host[i] = True  # undecodable alone: always check it on the host
+            tab = cache[stop_text] = host.to(self.device)
+        return tab
 
     # ---------------------------------------------------------------- protocol
     def encode_seed(self, text: str) -> List[int]:
@@ -251,30 +324,25 @@ class HipArithmeticLM:
         logits = self.lm.prefill(context, B, budget)
         if graphs is None:
             graphs = B <= GRAPH_MAX_BATCH
-        use_graph = (graphs and stop_text is None and getattr(self.lm, "hip_attention", False)
-                     and hasattr(self.lm, "begin_static"))
+        use_graph = graphs and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
         # token history: a captured graph needs a fixed buffer (the hard cap); the eager loop starts at the
         # KV budget and grows it at the host checks (at B = 4096 the hard cap alone would be 8.6 GB)
         sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap if use_graph else budget, stats=return_stats)
+        stop = _StopCheck(self, sess, stop_text) if stop_text is not None else None
+
+        def coder_step(lg):
+            tok = sess.step(lg, finish_sent=finish)
+            if stop is not None:
+                stop.flag(tok)  # device-side: did any live stream emit a token that can complete stop_text?
+            return tok
+
         t = 0
         last_pos = None
         last_move = 0
-        outs: List[List[int]] = [[] for _ in range(B)]
         graph = None
         while True:
-            if stop_text is not None and t > 0:
-                # code_base/arithmetic.py:207-210: a stream stops once its decoded cover text contains
-                # stop_text ('<eos>' in the message->bits mode of run_single.py).  Checked on a decoded tail.
-                f = sess.fields()
-                tok = sess.out_token.cpu().numpy()
-                stop = []
-                for i in range(B):
-                    if not (f["flags"][i] & 1) and len(outs[i]) < int(f["ntokens"][i]):
-                        outs[i].append(int(tok[i]))
-                        if stop_text in self.tokenizer.decode(outs[i][-16:]):
-                            stop.append(i)
-                if stop:
-                    sess.mark_done(stop)
+            if stop is not None and t > 0:
+                stop.check()  # code_base/arithmetic.py:207-210 ('<eos>' in run_single.py's message->bits mode)
             if t % check_every == 0:
                 f = sess.fields()
                 if bool((f["flags"] & 1).all()):
@@ -298,14 +366,14 @@ class HipArithmeticLM:
                         "has no underflow handling and would loop forever)")
             if use_graph and self.lm.static_capacity_left() >= 1:
                 if graph is None:
-                    graph = _StepGraph(self.lm, lambda lg: sess.step(lg, finish_sent=finish), logits)
+                    graph = _StepGraph(self.lm, coder_step, logits)
                 else:
                     graph.replay()
                 t += 1
                 continue
             if graph is not None:  # the preallocated cache is used up: continue eagerly (the cache grows)
                 logits, graph, use_graph = graph.logits, None, False
-            tok = sess.step(logits, finish_sent=finish)
+            tok = coder_step(logits)
             logits = self.lm.step(tok)
             t += 1
         del graph

@@ -76,12 +76,17 @@ class HipRankLM:
         self._decode_states: Deque[CodecState] = deque()
 
     def _coder(self, B: int) -> CoderContext:
-        ctx = self._ctx.get(B)
+        """One coder context (the parameters never change here) sized for the largest batch seen so far: a
+        smaller batch reuses it, a larger one replaces it (the kernels take B per call)."""
+        ctx = self._ctx.get(0)
+        if ctx is not None and ctx.max_batch < B:
+            ctx.close()
+            ctx = None
         if ctx is None:
             params = CoderParams(vocab=self.vocab, precision=16, temp=1.0, topk=self.vocab, dtype=self.logits_dtype,
                                  banned=[])
-            ctx = CoderContext(params, max_batch=B, device=self.device_index)
-            self._ctx[B] = ctx
+            ctx = CoderContext(params, max_batch=max(B, 1), device=self.device_index)
+            self._ctx[0] = ctx
         return ctx
 
     # ------------------------------------------------------------------ protocol (api.py:42-56)
