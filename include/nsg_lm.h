@@ -1,0 +1,63 @@
+/*
+ * nsg_lm.h -- batch-invariant decode-step kernels of the batched GPT-2 forward (row a19 of SURVEY.md §8),
+ * part of `libnsgcoder.so`.
+ *
+ * Replace, for the decode steps of the reference's per-token forward
+ * `model(prev, past_key_values=past, position_ids=...)` (code_base/arithmetic.py:115-122, Hugging Face
+ * GPT2Block: ln_1 -> c_attn -> attention -> c_proj (+ residual) -> ln_2 -> c_fc -> gelu_new -> c_proj
+ * (+ residual); ln_f; lm_head), the PyTorch/hipBLASLt ops whose per-row results depend on the batch size (the
+ * library picks a GEMM kernel per M).  The arithmetic coder needs the DECODER to see bit-identical logits to
+ * the ENCODER, and a cover made in a batch of B streams is often revealed alone (B = 1): every kernel here
+ * computes a row's result in an order that does not depend on M, on the row's position in the batch or on the
+ * tile shape chosen for M:
+ *
+ *   ns_lm_gemm       Y = epilogue(X . Wt^T + bias): one MFMA instruction (v_mfma_f32_16x16x32_f16) for every
+ *                    shape, output element (m, n) at MFMA position (n mod 16, m mod 16), K accumulated in
+ *                    ascending 32-wide steps into one fp32 chain, no split-K; the tile (16 x 16..64 direct
+ *                    loads for small M, 64x64 / 128x128 LDS tiles for large M) changes only WHICH wave
+ *                    computes an element, never how.
+ *   ns_lm_layernorm  one wavefront per row, fixed per-lane order + xor butterfly for mean and variance.
+ *   ns_lm_embed_ln   h = wte[token] + wpe[pos] (fp16) and ln_1(h) in one pass (pos = L mod n_positions,
+ *                    code_base/arithmetic.py:44-48; L from the host or from device memory for graph replays).
+ *
+ * fp16 operands, fp32 accumulation; no allocation; stream-ordered on the caller's hipStream_t.  Returns 0 or a
+ * negative NS_ERR_* code of nsg_coder.h.
+ */
+#ifndef NSG_LM_H
+#define NSG_LM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NS_LM_EPI_STORE 0    /* y = fp16(acc + bias)                                   */
+#define NS_LM_EPI_GELU 1     /* y = fp16(gelu_tanh(acc + bias))   (GPT-2 "gelu_new")   */
+#define NS_LM_EPI_RESIDUAL 2 /* y = fp16(y + (acc + bias)), in place (the residual add) */
+#define NS_LM_EPI_STORE_F32 3 /* y (fp32) = acc + bias                                   */
+
+/* d_x fp16 [M, ldx] (rows = streams), d_wt fp16 [N, ldw] (the weight TRANSPOSED: row n holds output column
+ * n's K coefficients), d_bias fp16 [N] or NULL, d_y [M, ldy] fp16 (fp32 for NS_LM_EPI_STORE_F32).  K must be a
+ * multiple of 64 and N a multiple of 16; rows 16-byte aligned (ldx, ldw multiples of 8 elements, ldy of 4). */
+int ns_lm_gemm(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
+               int64_t ldy, int M, int N, int K, int epilogue, void* hip_stream);
+
+/* d_x fp16 [M, ldx] -> d_y fp16 [M, ldy] = (x - mean) / sqrt(var + eps) * w + b per row; C % 4 == 0,
+ * C <= 2048. */
+int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy, int M,
+                    int C, float eps, void* hip_stream);
+
+/* d_tokens int32 [M]; d_wte fp16 [V, C]; d_wpe fp16 [n_positions, C]; position = L mod n_positions with
+ * L = *d_L (int32, device) when d_L is not NULL, else the host value.  Writes d_h fp16 [M, ldh] = wte + wpe
+ * and d_a fp16 [M, lda] = layernorm(h; w, b, eps).  Token ids outside [0, V) write NaN rows (the caller
+ * validates ids on the host; the kernel never reads outside the table). */
+int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions, int L,
+                   const int32_t* d_L, void* d_h, int64_t ldh, const void* d_w, const void* d_b, void* d_a,
+                   int64_t lda, int M, int C, float eps, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NSG_LM_H */

@@ -20,6 +20,10 @@
 
 namespace nsg {
 
+#ifndef NSG_ATT_SPLIT
+#define NSG_ATT_SPLIT 8  // waves per (stream, head) pair, for every batch size (measured: DESIGN.md §4b)
+#endif
+
 constexpr int ATT_D = 64;
 constexpr int ATT_WAVES = 4;  // (stream, head) pairs per 256-thread workgroup
 constexpr int ATT_U = 4;      // 8-row chunks per loop iteration: 32 keys per wave in flight
@@ -189,20 +193,21 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
     const float scale_log2 = scale * 1.4426950408889634f;
-    // waves per pair by batch size: a launch wants well over the chip's 256 CUs x a few waves
+    // The split (waves per (stream, head) pair) fixes the summation order of the softmax and of the output, so
+    // it is the SAME for every batch size: a stream's attention output -- and the logits the coder sees -- must
+    // not depend on how many other streams share the launch (a cover encoded at B = 4096 is decoded alone).
     const hipStream_t st = (hipStream_t)hip_stream;
     const _Float16* q = (const _Float16*)d_qkv;
     _Float16 *k = (_Float16*)d_k_cache, *v = (_Float16*)d_v_cache, *o = (_Float16*)d_out;
-    if (pairs <= 256)
-        hipLaunchKernelGGL(nsg::decode_attn_kernel<8>, dim3(pairs), dim3(64 * 8), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
-    else if (pairs <= 1024)
-        hipLaunchKernelGGL(nsg::decode_attn_kernel<4>, dim3(pairs), dim3(64 * 4), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
-    else
-        hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
-                           dim3(64 * nsg::ATT_WAVES), 0, st, q, qkv_stride, k, v, cache_b_stride, cache_h_stride, B,
-                           H, L0, d_L0, cap, o, out_stride, scale_log2);
+#if NSG_ATT_SPLIT > 1
+    hipLaunchKernelGGL(nsg::decode_attn_kernel<NSG_ATT_SPLIT>, dim3(pairs), dim3(64 * NSG_ATT_SPLIT), 0, st, q,
+                       qkv_stride, k, v, cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride,
+                       scale_log2);
+#else
+    hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
+                       dim3(64 * nsg::ATT_WAVES), 0, st, q, qkv_stride, k, v, cache_b_stride, cache_h_stride, B, H,
+                       L0, d_L0, cap, o, out_stride, scale_log2);
+#endif
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 

@@ -1,0 +1,424 @@
+// Batch-invariant decode-step kernels of the batched GPT-2 forward (include/nsg_lm.h).
+//
+// Reference semantics: Hugging Face GPT2Block / GPT2LMHeadModel for one new token per stream
+// (code_base/arithmetic.py:115-122).  What matters here beyond the semantics is that a stream's logits do not
+// depend on the batch it runs in: the arithmetic decoder must reproduce the encoder's integer CDF exactly,
+// and a cover encoded among B streams is revealed alone.
+//
+// GEMM: Y[m, n] = epi(sum_k X[m, k] * Wt[n, k] + bias[n]).  Every element is ONE fp32 accumulator chain of
+// v_mfma_f32_16x16x32_f16 over k = 0, 32, 64, ... with the weight row in MFMA row position n & 15 and the
+// activation row in MFMA column position m & 15 -- in every kernel variant.  The variants differ only in how
+// many elements a wave owns and how the operands reach the registers:
+//   * gemm_direct<FM>  (M <= 16 * FM, FM = 1, 2, 4): a wave owns 16 weight rows x 16*FM activation rows and
+//     loads its fragments straight from global memory (the weight row is read once; small batches are
+//     latency- and weight-bandwidth-bound, an LDS round trip would only add latency);
+//   * gemm_tiled<BN, BM>: a workgroup of 4 waves owns a BN x BM tile; both operands are staged into LDS with
+//     global_load_lds (16 B per lane, two buffers, counted vmcnt + raw s_barrier so the next K-tile's copy
+//     overlaps this one's MFMAs), rows 128 B long and XOR-swizzled by (row >> 1) & 7 in 16-B chunks so the
+//     16-lane groups of a ds_read_b128 hit distinct banks (the swizzle is applied to the global SOURCE
+//     address; the LDS image is written linearly by the DMA).  Workgroup ids are remapped so each XCD
+//     (private L2) runs a contiguous range of tiles that share weight panels.
+// The accumulator layout of the 16x16 MFMA puts four consecutive n of one m in a lane, so each lane stores
+// 8 bytes (fp16) or 16 bytes (fp32) per fragment and the bias is read as 4 consecutive values.
+//
+// LayerNorm: one wavefront per row; per-lane sums in a fixed order, xor butterfly (every lane ends with the
+// same bits); two-pass variance.  fp-contract is off for the whole library, so no FMA is formed implicitly.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nsg_coder.h"
+#include "nsg_lm.h"
+
+namespace nsg {
+namespace lm {
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;  // K per staged tile: 128-byte rows
+
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    // GPT-2 gelu_new: 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+    const float u = 0.7978845608028654f * (x + 0.044715f * (x * x * x));
+    return 0.5f * x * (1.0f + tanhf(u));
+}
+
+// Epilogue of one 16x16 fragment: lane holds n0..n0+3 of row m.
+template <int EPI>
+__device__ __forceinline__ void store4(void* Y, int64_t ldy, const f16* __restrict__ bias, int m, int n, f32x4 acc) {
+    float v[4];
+    if (bias) {
+        const f16x4 bb = *(const f16x4*)(bias + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[r] + (float)bb[r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[r];
+    }
+    if constexpr (EPI == NS_LM_EPI_STORE_F32) {
+        float* y = (float*)Y + (int64_t)m * ldy + n;
+        *(f32x4*)y = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+        f16* y = (f16*)Y + (int64_t)m * ldy + n;
+        f16x4 o;
+        if constexpr (EPI == NS_LM_EPI_RESIDUAL) {
+            const f16x4 h = *(const f16x4*)y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (f16)((float)h[r] + v[r]);
+        } else if constexpr (EPI == NS_LM_EPI_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (f16)gelu_tanh(v[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+        }
+        *(f16x4*)y = o;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------- direct
+// 4 waves per workgroup, wave w owns weight rows [16*(4*blockIdx.x + w), +16) and activation rows [0, 16*FM).
+template <int FM, int EPI>
+__global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
+                                                   int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
+                                                   int M, int N, int K) {
+    const int lane = threadIdx.x & 63;
+    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nb * 16 >= N) return;
+    const int r = lane & 15, c = lane >> 4;
+    const f16* wrow = Wt + (int64_t)min(nb * 16 + r, N - 1) * ldw + c * 8;
+    const f16* xrow[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) xrow[f] = X + (int64_t)min(f * 16 + r, M - 1) * ldx + c * 8;
+    f32x4 acc[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 8;  // 32-wide k-steps per batch of loads (K % 64 == 0 -> K/32 even)
+    int k = 0;
+    for (; k + 32 * U <= K; k += 32 * U) {
+        f16x8 a[U], b[U][FM];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = *(const f16x8*)(wrow + k + 32 * u);
+#pragma unroll
+            for (int f = 0; f < FM; ++f) b[u][f] = *(const f16x8*)(xrow[f] + k + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int f = 0; f < FM; ++f) acc[f] = mfma16(a[u], b[u][f], acc[f]);
+    }
+    for (; k < K; k += 32) {
+        const f16x8 a = *(const f16x8*)(wrow + k);
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[f] = mfma16(a, *(const f16x8*)(xrow[f] + k), acc[f]);
+    }
+    const int n = nb * 16 + 4 * c;
+    if (n >= N) return;
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+        const int m = f * 16 + r;
+        if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[f]);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------------- tiled
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+template <int N_>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
+    // s_waitcnt encoding (gfx9): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+    __builtin_amdgcn_s_waitcnt((N_ & 15) | (7 << 4) | (15 << 8) | ((N_ >> 4) << 14));
+}
+
+__device__ __forceinline__ void lds_fence_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// XCD-aware bijective remap: hardware dispatches workgroup i to XCD i % 8; give each XCD a contiguous range.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int q = nwg >> 3, rr = nwg & 7, x = bid & 7;
+    return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
+}
+
+template <int BN, int BM, int EPI>
+__global__ __launch_bounds__(256) void gemm_tiled(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
+                                                  int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
+                                                  int M, int N, int K) {
+    constexpr int WN = 2, WM = 2;                // 4 waves
+    constexpr int FN = BN / (16 * WN), FM = BM / (16 * WM);
+    constexpr int ROWS = BN + BM;                // staged rows per K-tile (weights first, then activations)
+    constexpr int GL = ROWS * 8 / 256;           // 16-byte DMA instructions per thread per K-tile
+    static_assert(ROWS * 8 % 256 == 0 && BN % 16 == 0 && BM % 16 == 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
+
+    const int tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int tn = t / tiles_m, tm = t - tn * tiles_m;  // m fastest: neighbouring tiles share a weight panel
+    const int n0 = tn * BN, m0 = tm * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wn = wave >> 1, wm = wave & 1;
+
+    // staging: instruction g of wave w fills LDS rows q*8 .. q*8+7, q = g*4 + w; lane -> row q*8 + lane/8,
+    // physical chunk lane%8, i.e. logical chunk (lane%8) ^ swz(row).
+    const f16* src[GL];
+    int lds_off[GL];
+#pragma unroll
+    for (int g = 0; g < GL; ++g) {
+        const int q = g * 4 + wave;
+        const int row = q * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ swz(row);
+        if (row < BN)
+            src[g] = Wt + (int64_t)min(n0 + row, N - 1) * ldw + chunk * 8;
+        else
+            src[g] = X + (int64_t)min(m0 + row - BN, M - 1) * ldx + chunk * 8;
+        lds_off[g] = q * 8 * 128;  // wave-uniform destination base; the DMA adds lane * 16
+    }
+    auto stage = [&](int kt, int buf) {
+#pragma unroll
+        for (int g = 0; g < GL; ++g)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[g] + kt * BK),
+                                             (__attribute__((address_space(3))) void*)(smem + buf * ROWS * 128 +
+                                                                                       lds_off[g]),
+                                             16, 0, 0);
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int KT = K / BK;
+    const int fr = lane & 15, fc = lane >> 4;
+    stage(0, 0);
+    for (int kt = 0; kt < KT; ++kt) {
+        if (kt + 1 < KT) {
+            stage(kt + 1, (kt + 1) & 1);
+            wait_vm<GL>();  // this thread's copies of tile kt have landed
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // ... and every other wave's
+        asm volatile("" ::: "memory");
+        const char* base = smem + (kt & 1) * ROWS * 128;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + fc;
+            f16x8 a[FN], b[FM];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int row = wn * FN * 16 + i * 16 + fr;
+                a[i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int row = BN + wm * FM * 16 + j * 16 + fr;
+                b[j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+        }
+        lds_fence_barrier();  // every wave is done reading buffer kt&1 before tile kt+2 is copied into it
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * FN * 16 + i * 16 + 4 * fc;
+        if (n >= N) continue;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int m = m0 + wm * FM * 16 + j * 16 + fr;
+            if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[i][j]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ layernorm
+constexpr int LN_MAXV = 8;  // f16x4 vectors per lane: C <= 2048
+
+__device__ __forceinline__ float wave_sum(float s) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+// Normalise the row held in x[] (NV4 = C/4 vectors, lane holds vectors lane, lane+64, ...), write fp16.
+__device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, const f16* __restrict__ w,
+                                       const f16* __restrict__ b, f16* __restrict__ y, float eps) {
+    const int lane = threadIdx.x & 63;
+    float s = 0.0f;
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v)
+        if (lane + 64 * v < NV4)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s += x[v][e];
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.0f;
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v)
+        if (lane + 64 * v < NV4)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = x[v][e] - mean;
+                q += d * d;
+            }
+    const float var = wave_sum(q) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v) {
+        const int i = lane + 64 * v;
+        if (i < NV4) {
+            const f16x4 ww = *(const f16x4*)(w + 4 * i);
+            const f16x4 bb = *(const f16x4*)(b + 4 * i);
+            f16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (f16)(((x[v][e] - mean) * rstd) * (float)ww[e] + (float)bb[e]);
+            *(f16x4*)(y + 4 * i) = o;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void layernorm_kernel(const f16* __restrict__ X, int64_t ldx,
+                                                        const f16* __restrict__ w, const f16* __restrict__ b,
+                                                        f16* __restrict__ Y, int64_t ldy, int M, int C, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int lane = threadIdx.x & 63, NV4 = C >> 2;
+    const f16* xr = X + (int64_t)row * ldx;
+    float x[LN_MAXV][4];
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v) {
+        const int i = lane + 64 * v;
+        if (i < NV4) {
+            const f16x4 t = *(const f16x4*)(xr + 4 * i);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[v][e] = (float)t[e];
+        }
+    }
+    ln_row(x, NV4, C, w, b, Y + (int64_t)row * ldy, eps);
+}
+
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict__ tokens, const f16* __restrict__ wte,
+                                                       const f16* __restrict__ wpe, int V, int n_positions, int L,
+                                                       const int32_t* __restrict__ dL, f16* __restrict__ H,
+                                                       int64_t ldh, const f16* __restrict__ w,
+                                                       const f16* __restrict__ b, f16* __restrict__ A, int64_t lda,
+                                                       int M, int C, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    if (dL) L = *dL;
+    const int pos = L % n_positions;  // code_base/arithmetic.py:44-48 (L >= 0)
+    const int lane = threadIdx.x & 63, NV4 = C >> 2;
+    const int tok = tokens[row];
+    const bool ok = tok >= 0 && tok < V;
+    const f16* er = wte + (int64_t)(ok ? tok : 0) * C;
+    const f16* pr = wpe + (int64_t)pos * C;
+    f16* hr = H + (int64_t)row * ldh;
+    float x[LN_MAXV][4];
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v) {
+        const int i = lane + 64 * v;
+        if (i < NV4) {
+            const f16x4 te = *(const f16x4*)(er + 4 * i);
+            const f16x4 tp = *(const f16x4*)(pr + 4 * i);
+            f16x4 h;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                h[e] = ok ? (f16)((float)te[e] + (float)tp[e]) : (f16)__builtin_nanf("");
+                x[v][e] = (float)h[e];
+            }
+            *(f16x4*)(hr + 4 * i) = h;
+        }
+    }
+    ln_row(x, NV4, C, w, b, A + (int64_t)row * lda, eps);
+}
+
+}  // namespace lm
+}  // namespace nsg
+
+using namespace nsg::lm;
+
+template <int EPI>
+static void launch_gemm(const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y, int64_t ldy,
+                        int M, int N, int K, hipStream_t st) {
+    if (M <= 64) {
+        const dim3 grid((N / 16 + 3) / 4), block(256);
+        if (M <= 16)
+            hipLaunchKernelGGL((gemm_direct<1, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
+        else if (M <= 32)
+            hipLaunchKernelGGL((gemm_direct<2, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
+        else
+            hipLaunchKernelGGL((gemm_direct<4, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
+        return;
+    }
+    const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
+    if (big >= 512) {
+        hipLaunchKernelGGL((gemm_tiled<128, 128, EPI>), dim3((unsigned)big), dim3(256), 0, st, x, ldx, wt, ldw, bias,
+                           y, ldy, M, N, K);
+    } else {
+        const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+        hipLaunchKernelGGL((gemm_tiled<64, 64, EPI>), dim3((unsigned)tiles), dim3(256), 0, st, x, ldx, wt, ldw, bias,
+                           y, ldy, M, N, K);
+    }
+}
+
+extern "C" int ns_lm_gemm(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
+                          int64_t ldy, int M, int N, int K, int epilogue, void* hip_stream) {
+    if (!d_x || !d_wt || !d_y || M <= 0 || N <= 0 || K <= 0) return NS_ERR_CONFIG;
+    if (K % 64 || N % 16) return NS_ERR_UNSUPPORTED;
+    if (ldx < K || ldw < K || ldy < N) return NS_ERR_CONFIG;
+    const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_wt | (uintptr_t)d_y | (uintptr_t)(d_bias ? d_bias : d_x);
+    if ((al & 15u) || (ldx & 7) || (ldw & 7) || (ldy & 3)) return NS_ERR_CONFIG;
+    if ((int64_t)M * ldx > 0x7FFFFFFFFFFFLL || (int64_t)((M + 127) / 128) * ((N + 127) / 128) > 0x7FFFFFFF)
+        return NS_ERR_UNSUPPORTED;
+    const f16 *x = (const f16*)d_x, *wt = (const f16*)d_wt, *b = (const f16*)d_bias;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    switch (epilogue) {
+        case NS_LM_EPI_STORE: launch_gemm<NS_LM_EPI_STORE>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_GELU: launch_gemm<NS_LM_EPI_GELU>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_RESIDUAL: launch_gemm<NS_LM_EPI_RESIDUAL>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_STORE_F32: launch_gemm<NS_LM_EPI_STORE_F32>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        default: return NS_ERR_CONFIG;
+    }
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
+                               int M, int C, float eps, void* hip_stream) {
+    if (!d_x || !d_w || !d_b || !d_y || M <= 0 || C <= 0) return NS_ERR_CONFIG;
+    if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
+    const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_w | (uintptr_t)d_b | (uintptr_t)d_y;
+    if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C) return NS_ERR_CONFIG;
+    hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, (const f16*)d_x,
+                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions,
+                              int L, const int32_t* d_L, void* d_h, int64_t ldh, const void* d_w, const void* d_b,
+                              void* d_a, int64_t lda, int M, int C, float eps, void* hip_stream) {
+    if (!d_tokens || !d_wte || !d_wpe || !d_h || !d_w || !d_b || !d_a || M <= 0 || C <= 0 || V <= 0 ||
+        n_positions <= 0 || (!d_L && L < 0))
+        return NS_ERR_CONFIG;
+    if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
+    const uintptr_t al = (uintptr_t)d_wte | (uintptr_t)d_wpe | (uintptr_t)d_h | (uintptr_t)d_w | (uintptr_t)d_b |
+                         (uintptr_t)d_a;
+    if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C) return NS_ERR_CONFIG;
+    hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
+                       (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, L, d_L, (f16*)d_h, ldh, (const f16*)d_w,
+                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}

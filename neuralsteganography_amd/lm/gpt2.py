@@ -9,11 +9,13 @@ forward semantics (``code_base/arithmetic.py:12-48,115-122``):
   (``_position_ids_for_cache``, ``:44-48``) and attends to the whole cache: the reference never truncates
   it (``limit_past`` slices head_dim, a no-op, ``code_base/utils.py:19-30``).
 
-Decode steps on the GPU in fp16 (the product configuration) run attention in the hand-written HIP kernel
-``ns_decode_attention`` (``csrc/nsg_attn.hip``: KV append fused with a one-pass online-softmax attention,
-one wavefront per (stream, head), HBM-bound on the cache); fp32 compute and the CPU keep PyTorch's
-``scaled_dot_product_attention`` as the forward's reference configuration (tests pin the two against each
-other and against Hugging Face).
+Decode steps on the GPU in fp16 (the product configuration) run entirely on hand-written HIP kernels whose
+per-stream results do not depend on the batch size (``include/nsg_lm.h``: MFMA GEMMs with the bias / gelu /
+residual epilogues fused, layer norms, embedding; ``include/nsg_attn.h``: KV append fused with a fixed-split
+online-softmax attention, HBM-bound on the cache), so a cover encoded in a batch of B streams decodes to the
+same logits alone.  The shared-context prefill (identical for encoder and decoder: one stream, T tokens),
+fp32 compute and the CPU keep PyTorch (``addmm`` + ``scaled_dot_product_attention``) as the forward's reference
+configuration (tests pin the two against each other and against Hugging Face).
 
 Logits are produced as ``h @ wte^T`` into a ``[B, ld]`` buffer with ``ld = row_stride(V)`` (zero weight
 columns beyond V), so the coder reads 16-byte-aligned rows without a copy.  Weights are taken from a
@@ -87,17 +89,27 @@ class BatchedGPT2:
         self.B = 0
         self.L = 0
         self.k_cache = self.v_cache = None
-        # decode-step attention: the HIP kernel for fp16 on the GPU (fails loudly if the library is missing)
-        self.hip_attention = self.device.type == "cuda" and self.dtype == torch.float16
-        if self.hip_attention:
+        # Decode steps in fp16 on the GPU run entirely on the batch-invariant HIP kernels (include/nsg_lm.h and
+        # the fixed-split attention of include/nsg_attn.h; fail loudly if the library is missing): a stream's
+        # logits are bit-identical whatever the batch it runs in, so a cover encoded among B streams decodes
+        # alone.  Weights are kept transposed ([N, K], K contiguous).  fp32 compute and the CPU keep the PyTorch
+        # path (SDPA), the forward's reference configuration in the tests.
+        self.native = self.device.type == "cuda" and self.dtype == torch.float16
+        self.hip_attention = self.native  # graph capture needs the native step (kept name: callers probe it)
+        self.d_L = None
+        self._static_logits = None
+        if self.native:
             from .. import _lib
 
             self._attn = _lib.lib().ns_decode_attention
             self._attn_dev = _lib.lib().ns_decode_attention_dev
             if self.shape.n_embd // self.shape.n_head != 64:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
-        self.d_L = None
-        self._static_logits = None
+            for lw in self.layers:
+                for name in ("qkv", "o", "fc", "pr"):
+                    lw[name + "_wt"] = lw[name + "_w"].t().contiguous()
+            self.head_t = self.head.t().contiguous()  # [ld, C]: wte rows, zero rows beyond V
+            self._nb = None
 
     # ------------------------------------------------------------------
     def kv_bytes_per_position(self, B: int) -> int:
@@ -114,6 +126,17 @@ class BatchedGPT2:
         if self.k_cache is not None:
             free += 2 * self.k_cache.numel() * self.k_cache.element_size()
         return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
+
+    def _native_buffers(self, B: int):
+        """Activation buffers of the native decode step (fixed addresses: a captured graph replays them)."""
+        if self._nb is None or self._nb["B"] != B:
+            C, dev, dt = self.shape.n_embd, self.device, self.dtype
+            self._nb = {"B": B, "h": torch.empty((B, C), device=dev, dtype=dt),
+                        "a": torch.empty((B, C), device=dev, dtype=dt),
+                        "qkv": torch.empty((B, 3 * C), device=dev, dtype=dt),
+                        "o": torch.empty((B, C), device=dev, dtype=dt),
+                        "f": torch.empty((B, 4 * C), device=dev, dtype=dt)}
+        return self._nb
 
     def allocate(self, B: int, max_len: int) -> None:
         s = self.shape
@@ -152,8 +175,6 @@ class BatchedGPT2:
         B, T, C = h.shape
         H, D = s.n_head, C // s.n_head
         a = self._ln(h, lw["ln1_w"], lw["ln1_b"])
-        if T == 1 and self.hip_attention and not causal:
-            return self._block_decode_hip(i, h, a)
         qkv = torch.addmm(lw["qkv_b"], a.reshape(B * T, C), lw["qkv_w"]).view(B, T, 3, H, D)
         q = qkv[:, :, 0].transpose(1, 2)
         k = qkv[:, :, 1].transpose(1, 2)
@@ -172,47 +193,6 @@ class BatchedGPT2:
         m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
         f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B * T, C), lw["fc_w"]), approximate="tanh")
         h = h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, T, C)
-        return h
-
-    def _block_decode_hip(self, i, h, a, dev_len: bool = False):
-        """One decode block with the fused KV-append + attention HIP kernel (``include/nsg_attn.h``); with
-        ``dev_len`` the cache length is read from ``self.d_L`` on the device (graph-capturable)."""
-        from ..coder import _stream_handle
-
-        s = self.shape
-        lw = self.layers[i]
-        B, _, C = h.shape
-        H, D = s.n_head, C // s.n_head
-        qkv = torch.addmm(lw["qkv_b"], a.reshape(B, C), lw["qkv_w"])  # [B, 3C] contiguous
-        o = torch.empty((B, C), device=h.device, dtype=self.dtype)
-        kc, vc = self.k_cache[i], self.v_cache[i]  # [Bmax, H, max_len, D]
-        if self.L >= kc.shape[2]:
-            raise RuntimeError("KV cache full")  # step() grows the cache before this point
-        if dev_len:
-            rc = self._attn_dev(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
-                                kc.stride(1), B, H, D, self.d_L.data_ptr(), kc.shape[2], o.data_ptr(), o.stride(0),
-                                1.0 / math.sqrt(D), _stream_handle())
-        else:
-            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
-                            B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), _stream_handle())
-        if rc != 0:
-            raise RuntimeError(f"ns_decode_attention failed ({rc})")
-        if B > 1:  # M > 1: the GEMM takes the bias in its epilogue; + residual is one add
-            h = h + torch.addmm(lw["o_b"], o, lw["o_w"]).view(B, 1, C)
-            m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
-            f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B, C), lw["fc_w"]), approximate="tanh")
-            return h + torch.addmm(lw["pr_b"], f, lw["pr_w"]).view(B, 1, C)
-        # M = 1 (the bias would be copied into the output first): residual adds in place -- bias into the
-        # residual stream, then the GEMM accumulates into it (beta = 1), two launches per projection instead of
-        # three (0.860 -> 0.814 ms/token at B = 1; at B = 64 this measured 2 % slower, hence the branch).  h is this
-        # step's own tensor (embedding sum or a previous block's output), never a captured graph input.
-        r = h.reshape(B, C)
-        if r.data_ptr() != h.data_ptr() or not r.is_contiguous():
-            raise RuntimeError("decode residual must be a contiguous [B, 1, C] tensor")
-        r.add_(lw["o_b"]).addmm_(o, lw["o_w"])
-        m = self._ln(h, lw["ln2_w"], lw["ln2_b"])
-        f = F.gelu(torch.addmm(lw["fc_b"], m.reshape(B, C), lw["fc_w"]), approximate="tanh")
-        r.add_(lw["pr_b"]).addmm_(f, lw["pr_w"])
         return h
 
     def _logits(self, h_last):
@@ -276,13 +256,76 @@ class BatchedGPT2:
         out = out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
         return out.view(B, T, self.ld)
 
+    def _decode_native(self, tokens: torch.Tensor, out: torch.Tensor, dev_len: bool) -> torch.Tensor:
+        """One decode step on the batch-invariant HIP kernels: embed + ln_1, then per layer c_attn GEMM, fused
+        KV-append attention, c_proj GEMM with the residual add in its epilogue, ln_2, c_fc GEMM with gelu_new in
+        its epilogue, c_proj GEMM + residual; ln_f and the head GEMM straight into ``out`` ([B, ld] logits).
+        ``dev_len``: the position / cache length come from ``self.d_L`` (graph replays)."""
+        from .. import _lib
+        from ..coder import _stream_handle
+
+        s = self.shape
+        B, C = self.B, s.n_embd
+        H, D = s.n_head, C // s.n_head
+        L = _lib.lib()
+        st = _stream_handle()
+        nb = self._native_buffers(B)
+        h, a, qkv, o, f = nb["h"], nb["a"], nb["qkv"], nb["o"], nb["f"]
+        tok = tokens if tokens.dtype == torch.int32 else tokens.to(torch.int32)
+        if not tok.is_contiguous() or tok.shape != (B,):
+            tok = tok.reshape(B).contiguous()
+        dL = self.d_L.data_ptr() if dev_len else None
+        if self.L >= self.k_cache.shape[3]:
+            raise RuntimeError("KV cache full")  # step() grows the cache before this point
+        eps = float(s.eps)
+
+        def ok(rc, what):
+            if rc != 0:
+                raise RuntimeError(f"{what} failed ({rc})")
+
+        def gemm(x, wt, bias, y, epi, N, K):
+            ok(L.ns_lm_gemm(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0),
+                            bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), B, N, K, epi,
+                            st), "ns_lm_gemm")
+
+        lw0 = self.layers[0]
+        ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
+                            self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
+                            a.data_ptr(), C, B, C, eps, st), "ns_lm_embed_ln")
+        for i, lw in enumerate(self.layers):
+            if i > 0:
+                ok(L.ns_lm_layernorm(h.data_ptr(), C, lw["ln1_w"].data_ptr(), lw["ln1_b"].data_ptr(), a.data_ptr(),
+                                     C, B, C, eps, st), "ns_lm_layernorm")
+            gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
+            kc, vc = self.k_cache[i], self.v_cache[i]
+            if dev_len:
+                rc = self._attn_dev(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                                    kc.stride(1), B, H, D, dL, kc.shape[2], o.data_ptr(), o.stride(0),
+                                    1.0 / math.sqrt(D), st)
+            else:
+                rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                                kc.stride(1), B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
+            ok(rc, "ns_decode_attention")
+            gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
+            ok(L.ns_lm_layernorm(h.data_ptr(), C, lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), a.data_ptr(), C,
+                                 B, C, eps, st), "ns_lm_layernorm")
+            gemm(a, lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C, C)
+            gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
+        ok(L.ns_lm_layernorm(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B, C,
+                             eps, st), "ns_lm_layernorm")
+        epi = _lib.NS_LM_EPI_STORE_F32 if out.dtype == torch.float32 else _lib.NS_LM_EPI_STORE
+        if out.shape != (B, self.ld) or out.stride(1) != 1:
+            raise ValueError(f"logits buffer must be [{B}, {self.ld}]")
+        gemm(a, self.head_t, None, out, epi, self.ld, C)
+        return out
+
     # ------------------------------------------------------------------ graph-capturable decode step
     def begin_static(self, logits_out: torch.Tensor) -> None:
         """Prepare :meth:`step_static`: the cache length moves to a device int32 (``d_L``) and the logits go to
         the fixed buffer ``logits_out`` ([B, ld]), so the same captured hipGraph replays every decode step.
         Needs the HIP attention path (fp16 on the GPU)."""
-        if not self.hip_attention:
-            raise RuntimeError("graph-captured decode steps need the HIP attention path (fp16 on the GPU)")
+        if not self.native:
+            raise RuntimeError("graph-captured decode steps need the native HIP step (fp16 on the GPU)")
         if logits_out.shape != (self.B, self.ld) or logits_out.dtype != self.logits_dtype:
             raise ValueError(f"static logits must be [{self.B}, {self.ld}] {self.logits_dtype}")
         self.d_L = torch.full((1,), self.L, dtype=torch.int32, device=self.device)
@@ -298,17 +341,7 @@ class BatchedGPT2:
         attention's cache length read from ``d_L``, logits written into the fixed buffer, ``d_L += 1``.  Issues
         no host synchronisation and no allocation that depends on the step, so it can be captured once.  The
         caller advances the host-side ``L`` by one per executed step."""
-        s = self.shape
-        pos = self.d_L.long() % s.n_positions
-        h = (self.wte.index_select(0, tokens.long()) + self.wpe.index_select(0, pos))[:, None, :]
-        for i in range(s.n_layer):
-            a = self._ln(h, self.layers[i]["ln1_w"], self.layers[i]["ln1_b"])
-            h = self._block_decode_hip(i, h, a, dev_len=True)
-        hf = self._ln(h[:, -1], self.lnf_w, self.lnf_b)
-        if self.logits_dtype == self.dtype:
-            torch.matmul(hf, self.head, out=self._static_logits)
-        else:
-            self._static_logits.copy_(hf @ self.head)
+        self._decode_native(tokens, self._static_logits, dev_len=True)
         self.d_L += 1
         return self._static_logits
 
@@ -320,6 +353,11 @@ class BatchedGPT2:
             self.grow(max(64, self.max_len))
         if tokens.shape != (B,):
             raise ValueError(f"expected {B} tokens")
+        if self.native:
+            out = torch.empty((B, self.ld), device=self.device, dtype=self.logits_dtype)
+            self._decode_native(tokens, out, dev_len=False)
+            self.L += 1
+            return out
         pos = self.L % self.shape.n_positions
         h = (self.wte[tokens.long()] + self.wpe[pos])[:, None, :]
         for i in range(self.shape.n_layer):

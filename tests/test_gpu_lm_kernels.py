@@ -1,0 +1,223 @@
+"""GPU: the batch-invariant decode-step kernels (include/nsg_lm.h, csrc/nsg_lm.hip; fixed-split attention of
+csrc/nsg_attn.hip).
+
+* numerics vs plain PyTorch fp32 references of the same ops (fp16 outputs: tolerances in each test);
+* batch invariance: a row's result is BIT-identical whatever M (and hence whichever kernel variant / tile and
+  position in the tile) computes it -- the property the arithmetic decoder needs (a cover encoded
+  among B streams is revealed alone);
+* end to end: fp16 GPT-2 logits of a stream equal bit for bit across batch sizes, and covers made with
+  cover_generate_batch at B > 1 in fp16 reveal one by one with cover_reveal.
+"""
+
+import math
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from neuralsteganography_amd import _lib, synthetic  # noqa: E402
+from neuralsteganography_amd.coder import _stream_handle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+EPIS = {"store": _lib.NS_LM_EPI_STORE, "gelu": _lib.NS_LM_EPI_GELU, "residual": _lib.NS_LM_EPI_RESIDUAL,
+        "f32": _lib.NS_LM_EPI_STORE_F32}
+
+
+def _gemm(x, wt, bias, y, epi):
+    M, K = x.shape
+    N = wt.shape[0]
+    rc = _lib.lib().ns_lm_gemm(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0),
+                               bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), M, N, K,
+                               EPIS[epi], _stream_handle())
+    assert rc == 0
+    return y
+
+
+def _ref(x, wt, bias, y0, epi):
+    acc = x.double() @ wt.double().t()
+    if bias is not None:
+        acc = acc + bias.double()
+    if epi == "gelu":
+        acc = 0.5 * acc * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (acc + 0.044715 * acc ** 3)))
+    if epi == "residual":
+        acc = y0.double() + acc
+    return acc
+
+
+def _operands(M, N, K, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn((M, K), generator=g, device="cuda").half()
+    wt = (torch.randn((N, K), generator=g, device="cuda") / math.sqrt(K)).half()
+    bias = (0.5 * torch.randn((N,), generator=g, device="cuda")).half()
+    return x, wt, bias
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 768, 768), (5, 2304, 768), (16, 64, 128), (17, 768, 3072), (33, 1024, 1024),
+                                   (64, 3072, 768), (65, 768, 768), (200, 2304, 768), (1000, 768, 3072),
+                                   (2048, 2048, 768), (4096, 2304, 768)])
+@pytest.mark.parametrize("epi", ["store", "gelu", "residual", "f32"])
+def test_gemm_matches_fp64_reference(M, N, K, epi):
+    """ns_lm_gemm vs float64 torch: fp32 accumulation of exact fp16 products, one fp16 rounding of the result
+    (2^-11 relative) -> |err| <= 2e-3 |ref| + 2e-3 on O(1) outputs."""
+    x, wt, bias = _operands(M, N, K, seed=M * 7 + N)
+    if epi == "f32":
+        y = torch.full((M, N), float("nan"), device="cuda")
+    elif epi == "residual":
+        y = torch.randn((M, N), device="cuda").half()
+    else:
+        y = torch.full((M, N), float("nan"), device="cuda").half()
+    y0 = y.clone()
+    use_bias = bias if (M + N) % 2 == 0 or epi != "store" else None
+    _gemm(x, wt, use_bias, y, epi)
+    torch.cuda.synchronize()
+    want = _ref(x, wt, use_bias, y0, epi)
+    err = (y.double() - want).abs()
+    assert torch.isfinite(y).all()
+    assert (err <= 2e-3 * want.abs() + 2e-3).all(), err.max().item()
+
+
+def test_gemm_ragged_leading_dims_and_rejections():
+    """Strided rows (ld > K / N) read and write only their own columns; bad shapes are refused, not launched."""
+    M, N, K = 70, 192, 256
+    x, wt, bias = _operands(M, N, K, seed=3)
+    xs = torch.zeros((M, K + 64), device="cuda").half()
+    xs[:, :K] = x
+    ys = torch.full((M, N + 8), 7.0, device="cuda").half()
+    _gemm(xs[:, :K], wt, bias, ys[:, :N], "store")
+    torch.cuda.synchronize()
+    assert torch.equal(ys[:, N:], torch.full((M, 8), 7.0, device="cuda").half())
+    want = _ref(x, wt, bias, None, "store")
+    assert ((ys[:, :N].double() - want).abs() <= 2e-3 * want.abs() + 2e-3).all()
+    f = _lib.lib().ns_lm_gemm
+    y = torch.empty((M, N), device="cuda").half()
+    assert f(x.data_ptr(), K, wt.data_ptr(), K, None, y.data_ptr(), N, M, N, 96, 0, None) == _lib.NS_ERR_UNSUPPORTED
+    assert f(x.data_ptr(), K, wt.data_ptr(), K, None, y.data_ptr(), N, M, 100, K, 0, None) == _lib.NS_ERR_UNSUPPORTED
+    assert f(x.data_ptr(), K, wt.data_ptr(), K, None, y.data_ptr(), N, M, N, K, 9, None) == _lib.NS_ERR_CONFIG
+    assert f(x.data_ptr(), K - 8, wt.data_ptr(), K, None, y.data_ptr(), N, M, N, K, 0, None) == _lib.NS_ERR_CONFIG
+
+
+@pytest.mark.parametrize("N,K,epi", [(2304, 768, "store"), (768, 3072, "residual"), (3072, 768, "gelu"),
+                                     (1024, 1024, "f32")])
+def test_gemm_rows_are_batch_invariant(N, K, epi):
+    """The same activation row gives the same output bits for every M (direct kernels M <= 16/32/64, 64x64 and
+    128x128 LDS tiles above) and every position of the row in its tile."""
+    Mbig = 4096
+    x, wt, bias = _operands(Mbig, N, K, seed=N + K)
+    ydt = torch.float32 if epi == "f32" else torch.float16
+    y0 = torch.randn((Mbig, N), device="cuda").to(ydt)
+    full = y0.clone()
+    _gemm(x, wt, bias, full, epi)
+    for M, off in [(1, 0), (1, 1234), (3, 7), (16, 100), (17, 31), (32, 5), (40, 2000), (64, 64), (65, 9),
+                   (300, 1), (1000, 1111), (2000, 3), (4000, 90)]:
+        y = y0[off:off + M].clone()
+        _gemm(x[off:off + M], wt, bias, y, epi)
+        torch.cuda.synchronize()
+        assert torch.equal(y, full[off:off + M]), (M, off)
+
+
+@pytest.mark.parametrize("M,C", [(1, 768), (7, 1024), (300, 768), (5, 64), (33, 1600)])
+def test_layernorm_matches_torch(M, C):
+    g = torch.Generator(device="cuda").manual_seed(M + C)
+    x = (3 * torch.randn((M, C), generator=g, device="cuda") + 1).half()
+    w = torch.randn((C,), generator=g, device="cuda").half()
+    b = torch.randn((C,), generator=g, device="cuda").half()
+    y = torch.full((M, C), float("nan"), device="cuda").half()
+    rc = _lib.lib().ns_lm_layernorm(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y.data_ptr(), C, M, C, 1e-5,
+                                    _stream_handle())
+    assert rc == 0
+    want = torch.nn.functional.layer_norm(x.float(), (C,), w.float(), b.float(), 1e-5)
+    assert ((y.float() - want).abs() <= 2e-3 * want.abs() + 4e-3).all()
+    # batch invariance: row 0 alone equals row 0 of the batch
+    y1 = torch.empty((1, C), device="cuda").half()
+    _lib.lib().ns_lm_layernorm(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y1.data_ptr(), C, 1, C, 1e-5,
+                               _stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(y1[0], y[0])
+
+
+@pytest.mark.parametrize("dev_len", [False, True])
+def test_embed_ln_matches_torch(dev_len):
+    V, P, C, M, L = 1000, 64, 256, 9, 70  # position = 70 % 64 = 6
+    g = torch.Generator(device="cuda").manual_seed(5)
+    wte = torch.randn((V, C), generator=g, device="cuda").half()
+    wpe = torch.randn((P, C), generator=g, device="cuda").half()
+    w = torch.randn((C,), generator=g, device="cuda").half()
+    b = torch.randn((C,), generator=g, device="cuda").half()
+    tok = torch.randint(0, V, (M,), generator=g, device="cuda", dtype=torch.int32)
+    h = torch.empty((M, C), device="cuda").half()
+    a = torch.empty((M, C), device="cuda").half()
+    dL = torch.tensor([L], dtype=torch.int32, device="cuda")
+    rc = _lib.lib().ns_lm_embed_ln(tok.data_ptr(), wte.data_ptr(), wpe.data_ptr(), V, P, -1 if dev_len else L,
+                                   dL.data_ptr() if dev_len else None, h.data_ptr(), C, w.data_ptr(), b.data_ptr(),
+                                   a.data_ptr(), C, M, C, 1e-5, _stream_handle())
+    assert rc == 0
+    want_h = wte[tok.long()] + wpe[L % P]
+    assert torch.equal(h, want_h)
+    want_a = torch.nn.functional.layer_norm(want_h.float(), (C,), w.float(), b.float(), 1e-5)
+    assert ((a.float() - want_a).abs() <= 2e-3 * want_a.abs() + 4e-3).all()
+
+
+def test_decode_attention_is_batch_invariant():
+    """The attention output of one (stream, head) is bit-identical at B = 1 and inside B = 700 (the split of a
+    pair's rows over waves no longer depends on the batch size)."""
+    B, H, D, L0 = 700, 12, 64, 333
+    g = torch.Generator(device="cuda").manual_seed(9)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kc = torch.randn((B, H, L0 + 8, D), generator=g, device="cuda").half()
+    vc = torch.randn((B, H, L0 + 8, D), generator=g, device="cuda").half()
+    f = _lib.lib().ns_decode_attention
+    out = torch.empty((B, H * D), device="cuda").half()
+    assert f(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), B, H, D, L0,
+             out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle()) == 0
+    for b in (0, 1, 399, 699):
+        o1 = torch.empty((1, H * D), device="cuda").half()
+        assert f(qkv[b:].data_ptr(), qkv.stride(0), kc[b:].data_ptr(), vc[b:].data_ptr(), kc.stride(0),
+                 kc.stride(1), 1, H, D, L0, o1.data_ptr(), o1.stride(0), D ** -0.5, _stream_handle()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o1[0], out[b]), b
+
+
+@pytest.mark.parametrize("logits", ["f16", "f32"])
+def test_gpt2_fp16_logits_are_batch_invariant(logits):
+    """GPT-2-small fp16 decode steps on the native kernels: every stream's logits at B = 37 equal, bit for bit,
+    the logits of the same stream run alone (B = 1) and inside a B = 5 batch, over several steps."""
+    from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+
+    m = random_gpt2("gpt2", seed=8)
+    ldt = torch.float16 if logits == "f16" else torch.float32
+    ctx = synthetic.DEFAULT_CONTEXT
+    g = torch.Generator().manual_seed(1)
+    steps = 4
+    toks = torch.randint(0, 50257, (steps, 37), generator=g)
+    big = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16, logits_dtype=ldt)
+    out_big = [big.prefill(ctx, 37, steps + 1)]
+    for t in range(steps):
+        out_big.append(big.step(toks[t].cuda()))
+    for rows in ([0], [36], [3, 10, 11, 20, 30]):
+        small = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16, logits_dtype=ldt)
+        out = [small.prefill(ctx, len(rows), steps + 1)]
+        for t in range(steps):
+            out.append(small.step(toks[t, rows].cuda()))
+        for t in range(steps + 1):
+            assert torch.equal(out[t], out_big[t][rows]), (rows, t)
+
+
+def test_fp16_cover_batch_reveals_alone():
+    """covers encoded with cover_generate_batch at B > 1 in fp16 -- the default on the GPU --
+    reveal one at a time with cover_reveal (B = 1), and the spans of a stego_encode_batch decode per message."""
+    from neuralsteganography_amd.cover import cover_generate_batch, cover_reveal
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from test_gpu_guard import IdTokenizer
+
+    m = random_gpt2("tiny", vocab_size=2000, n_positions=1024, n_embd=128, n_head=2, seed=23)
+    lm = HipArithmeticLM(m, IdTokenizer(2000), compute_dtype=torch.float16, logits_dtype="f16")
+    assert lm.lm.native
+    q = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": False}
+    secrets = [b"first secret", bytes(range(60)), b"z", b"another one, a little longer than the rest"]
+    seed = "w5. w6. w3"
+    texts = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="none", lm=lm, quality_gate=False,
+                                 chunk_bytes=24)
+    for text, secret in zip(texts, secrets):
+        assert cover_reveal(text, seed_text=seed, quality=q, ecc="none", lm=lm) == secret

@@ -228,17 +228,18 @@ def test_hip_decode_attention_rejects_bad_shapes():
              t.data_ptr(), 64, 0.1, None) == _lib.NS_ERR_CONFIG  # L0 beyond the cache capacity
 
 
-@pytest.mark.parametrize("B", [3, 1])  # B = 1: the in-place residual GEMMs and 8 attention waves per head
+@pytest.mark.parametrize("B", [3, 1])
 def test_gpt2_fp16_decode_hip_attention_matches_sdpa_and_hf(B):
-    """GPT-2-small fp16 decode steps: HIP attention path vs the SDPA path on identical weights (fp16 round-off
-    only), and the last step vs Hugging Face fp32 on CPU over the whole sequence (3e-2 absolute)."""
+    """GPT-2-small fp16 decode steps: the native HIP step (nsg_lm GEMMs / layer norms + HIP attention) vs the
+    PyTorch path on identical weights (fp16 round-off only), and the last step vs Hugging Face fp32 on CPU over
+    the whole sequence (3e-2 absolute)."""
     from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
 
     m = random_gpt2("gpt2", seed=5)
     a = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16)
     b = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16)
-    b.hip_attention = False
-    assert a.hip_attention
+    b.native = b.hip_attention = False  # the PyTorch decode path (hipBLASLt GEMMs + SDPA) on the same weights
+    assert a.native
     ctx = synthetic.DEFAULT_CONTEXT
     la, lb = a.prefill(ctx, B, 4), b.prefill(ctx, B, 4)
     toks = [[11, 500, 9000], [7, 7, 7], [42, 43, 44], [50000, 1, 2], [3, 4, 5], [9, 8, 7]]
