@@ -3,8 +3,9 @@
 // Reference semantics: Hugging Face GPT2Attention for one new token per stream over the unbounded cache the
 // reference keeps (code_base/arithmetic.py:115-122): softmax(q k^T / sqrt(D)) v over positions 0..L0.
 //
-// Layout: one wavefront per (stream, head) -- or, for small batches, a workgroup of 4 or 8 waves per pair that
-// split the rows and merge their partials through LDS (decode_attn_kernel<NSPLIT>).  Lane l holds dims 8*(l&7)..+7 of key row (l>>3) of an 8-row
+// Layout: a pair's rows are split over S = 1, 2, 4 or 8 waves by the KEY COUNT alone (att_split), so the
+// summation order -- and every output bit -- is the same whatever the batch size; the S partials are merged in
+// wave order through LDS.  Lane l holds dims 8*(l&7)..+7 of key row (l>>3) of an 8-row
 // chunk, so an 8-lane group reads one 128-byte K (and V) row and the wave reads 1 KiB of contiguous cache per
 // 16-byte load instruction.  Scores are reduced inside the 8-lane group; each group keeps its own online
 // softmax (running max, sum, 8 accumulator dims) over the rows it saw, and the 8 groups are merged once at the
@@ -20,12 +21,14 @@
 
 namespace nsg {
 
-#ifndef NSG_ATT_SPLIT
-#define NSG_ATT_SPLIT 8  // waves per (stream, head) pair, for every batch size (measured: DESIGN.md §4b)
+#ifndef NSG_ATT_ROWS1
+#define NSG_ATT_ROWS1 128  // keys per pair up to which one wave takes the whole pair (then 2, 4, 8 waves)
+#endif
+#ifndef NSG_ATT_SMALL_PAIRS
+#define NSG_ATT_SMALL_PAIRS 1024  // up to this many (stream, head) pairs: one pair per workgroup
 #endif
 
 constexpr int ATT_D = 64;
-constexpr int ATT_WAVES = 4;  // (stream, head) pairs per 256-thread workgroup
 constexpr int ATT_U = 4;      // 8-row chunks per loop iteration: 32 keys per wave in flight
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -45,133 +48,150 @@ __device__ __forceinline__ void unpack8(f16x8 v, float* f) {
     for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
 }
 
-// NSPLIT = 1: one wave per (stream, head), ATT_WAVES pairs per workgroup (large batches: enough waves).
-// NSPLIT > 1: one workgroup of NSPLIT waves per pair (small batches: a lone wave per pair leaves the chip
-// idle); wave w takes the 32-row chunks w, w + NSPLIT, ... and the NSPLIT online-softmax partials are merged
-// through LDS by wave 0 -- no cross-workgroup hand-off.
-template <int NSPLIT>
-__global__ __launch_bounds__(64 * (NSPLIT > 1 ? NSPLIT : ATT_WAVES)) void decode_attn_kernel(
-    const _Float16* __restrict__ qkv, int64_t qkv_stride, _Float16* kc, _Float16* vc, int64_t cb, int64_t ch, int B,
-    int H, int L0, const int32_t* __restrict__ L0p, int cap, _Float16* __restrict__ out, int64_t out_stride,
-    float scale_log2) {
+// Split of one (stream, head) pair's rows over waves, a function of the key count ONLY (never of the batch):
+// S waves take the 32-row chunks w, w + S, ... and their online-softmax partials are merged in wave order.
+// Short caches keep one wave per pair (a short row list split eight ways is mostly idle waves); long caches
+// use eight, so a lone stream still spreads its rows over a CU.
+__device__ __forceinline__ int att_split(int Lk) {
+    return Lk <= NSG_ATT_ROWS1 ? 1 : Lk <= 2 * NSG_ATT_ROWS1 ? 2 : Lk <= 4 * NSG_ATT_ROWS1 ? 4 : 8;
+}
+
+// Workgroup = 8 waves serving P consecutive pairs (P = 1 for small batches, 8 otherwise; P changes only which
+// workgroup computes a pair, not how).  With S = att_split(L0 + 1), the waves form 8/S groups of S; group
+// q takes pairs q, q + 8/S, ... of the workgroup, one round per pair, all waves running the same number of
+// rounds so the LDS merge's barriers are uniform.
+template <int P>
+__global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __restrict__ qkv, int64_t qkv_stride,
+                                                          _Float16* kc, _Float16* vc, int64_t cb, int64_t ch, int B,
+                                                          int H, int L0, const int32_t* __restrict__ L0p, int cap,
+                                                          _Float16* __restrict__ out, int64_t out_stride,
+                                                          float scale_log2) {
     if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
     if (L0 < 0 || L0 >= cap) return;                     // never write past the cache (host checks capacity)
+    __shared__ float s_m[8], s_l[8];
+    __shared__ float s_acc[8][ATT_D];
+    const int Lk = L0 + 1;
+    const int S = att_split(Lk);
     const int lane = threadIdx.x & 63;
-    const int wv = NSPLIT > 1 ? (int)(threadIdx.x >> 6) : 0;  // split index
-    const int pair = NSPLIT > 1 ? (int)blockIdx.x : (int)(blockIdx.x * ATT_WAVES + (threadIdx.x >> 6));
-    if (pair >= B * H) return;  // (NSPLIT > 1: uniform over the workgroup, before any barrier)
-    const int b = pair / H;
-    const int h = pair - b * H;
+    const int wave = threadIdx.x >> 6;
+    const int grp = wave / S, wv = wave - grp * S, ngrp = 8 / S;
     const int g = lane >> 3;  // row within an 8-row chunk
     const int c = lane & 7;   // 8-dim slice
     const int C = H * ATT_D;
-    const _Float16* qrow = qkv + (int64_t)b * qkv_stride + h * ATT_D + c * 8;
-    const f16x8 q = *(const f16x8*)qrow;
-    const f16x8 knew = *(const f16x8*)(qrow + C);
-    const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
-    _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
-    _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
-    if (g == 0 && wv == 0) {  // KV append of the new token (position L0)
-        *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
-        *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
-    }
-    const int Lk = L0 + 1;
     const int last_cached = L0 > 0 ? L0 - 1 : 0;
-    float m = -1e30f, l = 0.0f;
-    float acc[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
-
-    for (int j0 = wv * 8 * ATT_U; j0 < Lk; j0 += NSPLIT * 8 * ATT_U) {
-        f16x8 kr[ATT_U], vr[ATT_U];
-#pragma unroll
-        for (int u = 0; u < ATT_U; ++u) {
-            const int row = min(j0 + 8 * u + g, last_cached);
-            kr[u] = __builtin_nontemporal_load((const f16x8*)(kb + (int64_t)row * ATT_D));
-            vr[u] = __builtin_nontemporal_load((const f16x8*)(vb + (int64_t)row * ATT_D));
-        }
-        float s[ATT_U];
-        bool valid[ATT_U];
-        float mx = m;
-#pragma unroll
-        for (int u = 0; u < ATT_U; ++u) {
-            const int row = j0 + 8 * u + g;
-            valid[u] = row < Lk;
-            if (row == L0) {  // the new token: from registers, not from the cache just written
-                kr[u] = knew;
-                vr[u] = vnew;
-            }
-            float sv = dot8(q, kr[u]);
-            sv += __shfl_xor(sv, 1);
-            sv += __shfl_xor(sv, 2);
-            sv += __shfl_xor(sv, 4);
-            s[u] = sv * scale_log2;
-            if (valid[u]) mx = fmaxf(mx, s[u]);
-        }
-        const float alpha = exp2f(m - mx);
-        l *= alpha;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) acc[d] *= alpha;
-#pragma unroll
-        for (int u = 0; u < ATT_U; ++u) {
-            const float p = valid[u] ? exp2f(s[u] - mx) : 0.0f;
-            l += p;
-            float v[8];
-            unpack8(vr[u], v);
-#pragma unroll
-            for (int d = 0; d < 8; ++d) acc[d] = fmaf(p, v[d], acc[d]);
-        }
-        m = mx;
-    }
-    // merge the 8 row groups (lanes c, c+8, ..., c+56 hold the same dims)
-#pragma unroll
-    for (int off = 8; off < 64; off <<= 1) {
-        const float mo = __shfl_xor(m, off);
-        const float lo = __shfl_xor(l, off);
-        const float mn = fmaxf(m, mo);
-        const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
-        l = l * fa + lo * fo;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            const float ao = __shfl_xor(acc[d], off);
-            acc[d] = acc[d] * fa + ao * fo;
-        }
-        m = mn;
-    }
-    if constexpr (NSPLIT > 1) {
-        // every lane now holds its wave's merged (m, l) and the 8 dims of slice c: waves 1.. hand theirs to wave 0
-        __shared__ float s_m[NSPLIT], s_l[NSPLIT];
-        __shared__ float s_acc[NSPLIT][ATT_D];
-        if (g == 0) {
-#pragma unroll
-            for (int d = 0; d < 8; ++d) s_acc[wv][c * 8 + d] = acc[d];
-            if (c == 0) {
-                s_m[wv] = m;
-                s_l[wv] = l;
-            }
-        }
-        __syncthreads();
-        if (wv != 0) return;
-        float mt = s_m[0];
-#pragma unroll
-        for (int w = 1; w < NSPLIT; ++w) mt = fmaxf(mt, s_m[w]);
-        l = 0.0f;
+    const int rounds = (P + ngrp - 1) / ngrp;
+    for (int rd = 0; rd < rounds; ++rd) {
+        const int j = grp + rd * ngrp;
+        const int pair = blockIdx.x * P + j;
+        const bool active = j < P && pair < B * H;  // uniform per wave group
+        float m = -1e30f, l = 0.0f;
+        float acc[8];
 #pragma unroll
         for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+        int b = 0, h = 0;
+        if (active) {
+            b = pair / H;
+            h = pair - b * H;
+            const _Float16* qrow = qkv + (int64_t)b * qkv_stride + h * ATT_D + c * 8;
+            const f16x8 q = *(const f16x8*)qrow;
+            const f16x8 knew = *(const f16x8*)(qrow + C);
+            const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
+            _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
+            _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
+            if (g == 0 && wv == 0) {  // KV append of the new token (position L0)
+                *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
+                *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
+            }
+            for (int j0 = wv * 8 * ATT_U; j0 < Lk; j0 += S * 8 * ATT_U) {
+                f16x8 kr[ATT_U], vr[ATT_U];
 #pragma unroll
-        for (int w = 0; w < NSPLIT; ++w) {
-            const float f = exp2f(s_m[w] - mt);
-            l += s_l[w] * f;
+                for (int u = 0; u < ATT_U; ++u) {
+                    const int row = min(j0 + 8 * u + g, last_cached);
+                    kr[u] = __builtin_nontemporal_load((const f16x8*)(kb + (int64_t)row * ATT_D));
+                    vr[u] = __builtin_nontemporal_load((const f16x8*)(vb + (int64_t)row * ATT_D));
+                }
+                float sc[ATT_U];
+                bool valid[ATT_U];
+                float mx = m;
 #pragma unroll
-            for (int d = 0; d < 8; ++d) acc[d] += s_acc[w][c * 8 + d] * f;
+                for (int u = 0; u < ATT_U; ++u) {
+                    const int row = j0 + 8 * u + g;
+                    valid[u] = row < Lk;
+                    if (row == L0) {  // the new token: from registers, not from the cache just written
+                        kr[u] = knew;
+                        vr[u] = vnew;
+                    }
+                    float sv = dot8(q, kr[u]);
+                    sv += __shfl_xor(sv, 1);
+                    sv += __shfl_xor(sv, 2);
+                    sv += __shfl_xor(sv, 4);
+                    sc[u] = sv * scale_log2;
+                    if (valid[u]) mx = fmaxf(mx, sc[u]);
+                }
+                const float alpha = exp2f(m - mx);
+                l *= alpha;
+#pragma unroll
+                for (int d = 0; d < 8; ++d) acc[d] *= alpha;
+#pragma unroll
+                for (int u = 0; u < ATT_U; ++u) {
+                    const float p = valid[u] ? exp2f(sc[u] - mx) : 0.0f;
+                    l += p;
+                    float v[8];
+                    unpack8(vr[u], v);
+#pragma unroll
+                    for (int d = 0; d < 8; ++d) acc[d] = fmaf(p, v[d], acc[d]);
+                }
+                m = mx;
+            }
+            // merge the 8 row groups (lanes c, c+8, ..., c+56 hold the same dims)
+#pragma unroll
+            for (int off = 8; off < 64; off <<= 1) {
+                const float mo = __shfl_xor(m, off);
+                const float lo = __shfl_xor(l, off);
+                const float mn = fmaxf(m, mo);
+                const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
+                l = l * fa + lo * fo;
+#pragma unroll
+                for (int d = 0; d < 8; ++d) {
+                    const float ao = __shfl_xor(acc[d], off);
+                    acc[d] = acc[d] * fa + ao * fo;
+                }
+                m = mn;
+            }
         }
-    }
-    if (g == 0) {
-        const float inv = 1.0f / l;
-        f16x8 w;
+        if (S > 1) {  // uniform over the workgroup: hand the S partials of each group to its first wave
+            if (active && g == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] = (_Float16)(acc[i] * inv);
-        *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * 8) = w;
+                for (int d = 0; d < 8; ++d) s_acc[wave][c * 8 + d] = acc[d];
+                if (c == 0) {
+                    s_m[wave] = m;
+                    s_l[wave] = l;
+                }
+            }
+            __syncthreads();
+            if (active && wv == 0) {
+                const int w0 = grp * S;
+                float mt = s_m[w0];
+                for (int w = 1; w < S; ++w) mt = fmaxf(mt, s_m[w0 + w]);
+                l = 0.0f;
+#pragma unroll
+                for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+                for (int w = 0; w < S; ++w) {
+                    const float f = exp2f(s_m[w0 + w] - mt);
+                    l += s_l[w0 + w] * f;
+#pragma unroll
+                    for (int d = 0; d < 8; ++d) acc[d] += s_acc[w0 + w][c * 8 + d] * f;
+                }
+            }
+            __syncthreads();  // the LDS slots are reused by the next round
+        }
+        if (active && wv == 0 && g == 0) {
+            const float inv = 1.0f / l;
+            f16x8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (_Float16)(acc[i] * inv);
+            *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * 8) = o;
+        }
     }
 }
 
@@ -193,21 +213,18 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
     const float scale_log2 = scale * 1.4426950408889634f;
-    // The split (waves per (stream, head) pair) fixes the summation order of the softmax and of the output, so
-    // it is the SAME for every batch size: a stream's attention output -- and the logits the coder sees -- must
-    // not depend on how many other streams share the launch (a cover encoded at B = 4096 is decoded alone).
+    // The row split per pair (att_split) depends on the key count only, so a stream's output -- and the logits the
+    // coder sees -- does not depend on how many other streams share the launch (a cover encoded at B = 4096 is
+    // decoded alone).  Pairs per workgroup follow the batch: 8 when there are enough pairs to fill the chip.
     const hipStream_t st = (hipStream_t)hip_stream;
     const _Float16* q = (const _Float16*)d_qkv;
     _Float16 *k = (_Float16*)d_k_cache, *v = (_Float16*)d_v_cache, *o = (_Float16*)d_out;
-#if NSG_ATT_SPLIT > 1
-    hipLaunchKernelGGL(nsg::decode_attn_kernel<NSG_ATT_SPLIT>, dim3(pairs), dim3(64 * NSG_ATT_SPLIT), 0, st, q,
-                       qkv_stride, k, v, cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride,
-                       scale_log2);
-#else
-    hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3((pairs + nsg::ATT_WAVES - 1) / nsg::ATT_WAVES),
-                       dim3(64 * nsg::ATT_WAVES), 0, st, q, qkv_stride, k, v, cache_b_stride, cache_h_stride, B, H,
-                       L0, d_L0, cap, o, out_stride, scale_log2);
-#endif
+    if (pairs <= NSG_ATT_SMALL_PAIRS)
+        hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
+                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
+    else
+        hipLaunchKernelGGL(nsg::decode_attn_kernel<8>, dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k, v,
+                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 

@@ -158,10 +158,11 @@ def test_embed_ln_matches_torch(dev_len):
     assert ((a.float() - want_a).abs() <= 2e-3 * want_a.abs() + 4e-3).all()
 
 
-def test_decode_attention_is_batch_invariant():
-    """The attention output of one (stream, head) is bit-identical at B = 1 and inside B = 700 (the split of a
-    pair's rows over waves no longer depends on the batch size)."""
-    B, H, D, L0 = 700, 12, 64, 333
+@pytest.mark.parametrize("L0", [0, 5, 127, 128, 255, 333, 700])  # one, two, four and eight waves per pair
+def test_decode_attention_is_batch_invariant(L0):
+    """The attention output of one (stream, head) is bit-identical at B = 1 (one pair per workgroup) and inside
+    B = 700 (eight pairs per workgroup): the split of a pair's rows over waves depends on the key count only."""
+    B, H, D = 700, 12, 64
     g = torch.Generator(device="cuda").manual_seed(9)
     qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
     kc = torch.randn((B, H, L0 + 8, D), generator=g, device="cuda").half()
