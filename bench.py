@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
     ap.add_argument("--e2e-eager", action="store_true", help="per-token launches instead of the captured hipGraph")
+    ap.add_argument("--e2e-kv-cap", type=int, default=None,
+                    help="cap the initial per-stream KV cache length (positions; it still grows on demand)")
     ap.add_argument("--blas", default=None, choices=["rocblas", "hipblaslt"],
                     help="GEMM library for the GPT-2 forward (torch.backends.cuda.preferred_blas_library)")
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
@@ -161,6 +163,7 @@ def end_to_end(args, rank, world, dev):
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
                          max_batch=B)
+    lm.lm.position_cap = args.e2e_kv_cap
     quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
     context = synthetic.DEFAULT_CONTEXT
     # warm-up: GEMM heuristics, kernels and the coder context at the same batch, short payloads

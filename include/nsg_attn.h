@@ -41,6 +41,18 @@ int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
                             int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, const int32_t* d_L0,
                             int cap, void* d_out, int64_t out_stride, float scale, void* hip_stream);
 
+/* The general form: positions [0, T0) are a prefix SHARED by all B streams (the common context, stored once:
+ * element (h, j, d) at h*prefix_h_stride + j*D + d, j < T0), positions [T0, L0] are the stream's own rows at
+ * index j - T0 of d_k_cache / d_v_cache (element (b, h, j - T0, d)).  `cap` = total positions (prefix + the
+ * stream cache's rows); the new token is written at stream index L0 - T0.  L0 comes from *d_L0 when d_L0 is not
+ * NULL (graph replays), else from the argument.  T0 = 0 is ns_decode_attention(_dev).  The output bits do not
+ * depend on where a row is stored (same values, same order). */
+int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                               int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
+                               const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
+                               const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
+                               void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,14 @@ extern "C" {
 int ns_lm_gemm(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
                int64_t ldy, int M, int N, int K, int epilogue, void* hip_stream);
 
+/* ns_lm_gemm with a forced tile configuration 0 <= config < ns_lm_gemm_configs() (-1 = the automatic choice):
+ * direct 16/32/64-row waves, 64x64 / 128x128 / 256x128 / 128x256 LDS tiles with 2-4 stages.  Every
+ * configuration produces the same bits (the batch-invariance contract); the choice is speed only (tuning and
+ * tests). */
+int ns_lm_gemm_config(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
+                      int64_t ldy, int M, int N, int K, int epilogue, int config, void* hip_stream);
+int ns_lm_gemm_configs(void);
+
 /* d_x fp16 [M, ldx] -> d_y fp16 [M, ldy] = (x - mean) / sqrt(var + eps) * w + b per row; C % 4 == 0,
  * C <= 2048. */
 int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy, int M,

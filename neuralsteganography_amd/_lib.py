@@ -28,8 +28,9 @@ NS_MAX_BANNED = 8
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
-           "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev",
-           "ns_score_rows", "ns_lm_gemm", "ns_lm_layernorm", "ns_lm_embed_ln")
+           "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
+           "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
+           "ns_lm_embed_ln")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
 
 
@@ -123,8 +124,15 @@ def lib() -> ctypes.CDLL:
     L.ns_decode_attention.argtypes = [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_float, vp]
     i64, ci = ctypes.c_int64, ctypes.c_int
+    L.ns_decode_attention_prefix.restype = ci
+    L.ns_decode_attention_prefix.argtypes = [vp, i64, vp, vp, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, vp,
+                                             i64, ctypes.c_float, vp]
     L.ns_lm_gemm.restype = ci
     L.ns_lm_gemm.argtypes = [vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, ci, vp]
+    L.ns_lm_gemm_config.restype = ci
+    L.ns_lm_gemm_config.argtypes = [vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp]
+    L.ns_lm_gemm_configs.restype = ci
+    L.ns_lm_gemm_configs.argtypes = []
     L.ns_lm_layernorm.restype = ci
     L.ns_lm_layernorm.argtypes = [vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
     L.ns_lm_embed_ln.restype = ci

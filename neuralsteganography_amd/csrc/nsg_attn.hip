@@ -60,14 +60,19 @@ __device__ __forceinline__ int att_split(int Lk) {
 // workgroup computes a pair, not how).  With S = att_split(L0 + 1), the waves form 8/S groups of S; group
 // q takes pairs q, q + 8/S, ... of the workgroup, one round per pair, all waves running the same number of
 // rounds so the LDS merge's barriers are uniform.
+// Positions [0, T0) come from a prefix shared by every stream (kp/vp, head stride ph: the common context,
+// stored once), positions [T0, L0] from the stream's own cache at index position - T0.  Same values, same
+// order: the output bits do not depend on where a row is stored.
 template <int P>
 __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __restrict__ qkv, int64_t qkv_stride,
-                                                          _Float16* kc, _Float16* vc, int64_t cb, int64_t ch, int B,
+                                                          _Float16* kc, _Float16* vc, int64_t cb, int64_t ch,
+                                                          const _Float16* __restrict__ kp,
+                                                          const _Float16* __restrict__ vp, int64_t ph, int T0, int B,
                                                           int H, int L0, const int32_t* __restrict__ L0p, int cap,
                                                           _Float16* __restrict__ out, int64_t out_stride,
                                                           float scale_log2) {
     if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
-    if (L0 < 0 || L0 >= cap) return;                     // never write past the cache (host checks capacity)
+    if (L0 < T0 || L0 >= cap) return;                    // never write past the cache (host checks capacity)
     __shared__ float s_m[8], s_l[8];
     __shared__ float s_acc[8][ATT_D];
     const int Lk = L0 + 1;
@@ -96,8 +101,11 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
             const f16x8 q = *(const f16x8*)qrow;
             const f16x8 knew = *(const f16x8*)(qrow + C);
             const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
-            _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
-            _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8;
+            // stream rows are addressed by position (index position - T0 folded into the base)
+            _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8 - (int64_t)T0 * ATT_D;
+            _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8 - (int64_t)T0 * ATT_D;
+            const _Float16* kpb = kp + (int64_t)h * ph + c * 8;
+            const _Float16* vpb = vp + (int64_t)h * ph + c * 8;
             if (g == 0 && wv == 0) {  // KV append of the new token (position L0)
                 *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
                 *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
@@ -107,8 +115,11 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
 #pragma unroll
                 for (int u = 0; u < ATT_U; ++u) {
                     const int row = min(j0 + 8 * u + g, last_cached);
-                    kr[u] = __builtin_nontemporal_load((const f16x8*)(kb + (int64_t)row * ATT_D));
-                    vr[u] = __builtin_nontemporal_load((const f16x8*)(vb + (int64_t)row * ATT_D));
+                    const bool pre = row < T0;
+                    const _Float16* ka = (pre ? kpb : kb) + (int64_t)row * ATT_D;
+                    const _Float16* va = (pre ? vpb : vb) + (int64_t)row * ATT_D;
+                    kr[u] = __builtin_nontemporal_load((const f16x8*)ka);
+                    vr[u] = __builtin_nontemporal_load((const f16x8*)va);
                 }
                 float sc[ATT_U];
                 bool valid[ATT_U];
@@ -198,18 +209,24 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
 }  // namespace nsg
 
 static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
-                            int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
+                            int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
+                            const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
                             const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
                             void* hip_stream) {
-    if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0) return NS_ERR_CONFIG;
+    if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0 || T0 < 0) return NS_ERR_CONFIG;
     if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
-    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_k_cache | (uintptr_t)d_v_cache | (uintptr_t)d_out;
+    if (T0 > 0 && (!d_k_prefix || !d_v_prefix || prefix_h_stride < (int64_t)T0 * D || (prefix_h_stride & 7)))
+        return NS_ERR_CONFIG;
+    if (!d_L0 && L0 < T0) return NS_ERR_CONFIG;
+    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_k_cache | (uintptr_t)d_v_cache | (uintptr_t)d_out |
+                            (uintptr_t)(T0 > 0 ? d_k_prefix : d_qkv) | (uintptr_t)(T0 > 0 ? d_v_prefix : d_qkv);
     if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || (cache_b_stride & 7) || (cache_h_stride & 7))
         return NS_ERR_CONFIG;  // 16-byte rows
     if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
-    if (cache_h_stride < (int64_t)(L0 + 1) * D || cache_h_stride < (int64_t)cap * D ||
-        cache_b_stride < (int64_t)H * cache_h_stride)
+    // the stream cache holds positions [T0, cap): cap - T0 rows per (stream, head)
+    if (cap <= T0 || cache_h_stride < (int64_t)(cap - T0) * D || cache_b_stride < (int64_t)H * cache_h_stride)
         return NS_ERR_CONFIG;
+    if (!d_L0 && L0 >= cap) return NS_ERR_CONFIG;
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
     const float scale_log2 = scale * 1.4426950408889634f;
@@ -219,20 +236,24 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     const hipStream_t st = (hipStream_t)hip_stream;
     const _Float16* q = (const _Float16*)d_qkv;
     _Float16 *k = (_Float16*)d_k_cache, *v = (_Float16*)d_v_cache, *o = (_Float16*)d_out;
+    const _Float16* kp = T0 > 0 ? (const _Float16*)d_k_prefix : k;
+    const _Float16* vp = T0 > 0 ? (const _Float16*)d_v_prefix : v;
     if (pairs <= NSG_ATT_SMALL_PAIRS)
         hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
+                           cache_b_stride, cache_h_stride, kp, vp, prefix_h_stride, T0, B, H, L0, d_L0, cap, o,
+                           out_stride, scale_log2);
     else
         hipLaunchKernelGGL(nsg::decode_attn_kernel<8>, dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, B, H, L0, d_L0, cap, o, out_stride, scale_log2);
+                           cache_b_stride, cache_h_stride, kp, vp, prefix_h_stride, T0, B, H, L0, d_L0, cap, o,
+                           out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
 extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                                    int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
                                    void* d_out, int64_t out_stride, float scale, void* hip_stream) {
-    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, B, H, D, L0,
-                            nullptr, L0 + 1, d_out, out_stride, scale, hip_stream);
+    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, nullptr, nullptr,
+                            0, 0, B, H, D, L0, nullptr, L0 + 1, d_out, out_stride, scale, hip_stream);
 }
 
 extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
@@ -240,6 +261,16 @@ extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, vo
                                        const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
                                        void* hip_stream) {
     if (!d_L0 || cap < 1) return NS_ERR_CONFIG;
-    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, B, H, D, 0,
-                            d_L0, cap, d_out, out_stride, scale, hip_stream);
+    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, nullptr, nullptr,
+                            0, 0, B, H, D, 0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+}
+
+extern "C" int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                                          int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
+                                          const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H,
+                                          int D, int L0, const int32_t* d_L0, int cap, void* d_out,
+                                          int64_t out_stride, float scale, void* hip_stream) {
+    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, d_k_prefix,
+                            d_v_prefix, prefix_h_stride, T0, B, H, D, d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride,
+                            scale, hip_stream);
 }

@@ -84,7 +84,8 @@ __device__ __forceinline__ void store4(void* Y, int64_t ldy, const f16* __restri
 }
 
 // ---------------------------------------------------------------------------------------------------- direct
-// 4 waves per workgroup, wave w owns weight rows [16*(4*blockIdx.x + w), +16) and activation rows [0, 16*FM).
+// 4 waves per workgroup, wave w owns weight rows [16*(4*blockIdx.x + w), +16) and activation rows
+// [16*FM*blockIdx.y, +16*FM).
 template <int FM, int EPI>
 __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
                                                    int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
@@ -92,11 +93,12 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
     const int lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (nb * 16 >= N) return;
+    const int m0 = blockIdx.y * 16 * FM;
     const int r = lane & 15, c = lane >> 4;
     const f16* wrow = Wt + (int64_t)min(nb * 16 + r, N - 1) * ldw + c * 8;
     const f16* xrow[FM];
 #pragma unroll
-    for (int f = 0; f < FM; ++f) xrow[f] = X + (int64_t)min(f * 16 + r, M - 1) * ldx + c * 8;
+    for (int f = 0; f < FM; ++f) xrow[f] = X + (int64_t)min(m0 + f * 16 + r, M - 1) * ldx + c * 8;
     f32x4 acc[FM];
 #pragma unroll
     for (int f = 0; f < FM; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
     if (n >= N) return;
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
-        const int m = f * 16 + r;
+        const int m = m0 + f * 16 + r;
         if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[f]);
     }
 }
@@ -151,16 +153,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
 }
 
-template <int BN, int BM, int EPI>
-__global__ __launch_bounds__(256) void gemm_tiled(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
-                                                  int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
-                                                  int M, int N, int K) {
-    constexpr int WN = 2, WM = 2;                // 4 waves
+template <int BN, int BM, int WN, int WM, int NST, int EPI>
+__global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict__ X, int64_t ldx,
+                                                            const f16* __restrict__ Wt, int64_t ldw,
+                                                            const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
+                                                            int N, int K) {
+    constexpr int NT = 64 * WN * WM;
+    constexpr int NW = WN * WM;
     constexpr int FN = BN / (16 * WN), FM = BM / (16 * WM);
     constexpr int ROWS = BN + BM;                // staged rows per K-tile (weights first, then activations)
-    constexpr int GL = ROWS * 8 / 256;           // 16-byte DMA instructions per thread per K-tile
-    static_assert(ROWS * 8 % 256 == 0 && BN % 16 == 0 && BM % 16 == 0, "tile shape");
-    __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
+    constexpr int GL = ROWS * 8 / NT;            // 16-byte DMA instructions per thread per K-tile
+    static_assert(ROWS * 8 % NT == 0 && BN % (16 * WN) == 0 && BM % (16 * WM) == 0 && BN % 16 == 0, "tile shape");
+    static_assert(NST >= 2 && NST <= 4, "stages");
+    __shared__ __attribute__((aligned(16))) char smem[NST * ROWS * 128];
 
     const int tiles_m = (M + BM - 1) / BM;
     const int tiles_n = (N + BN - 1) / BN;
@@ -168,15 +173,15 @@ __global__ __launch_bounds__(256) void gemm_tiled(const f16* __restrict__ X, int
     const int tn = t / tiles_m, tm = t - tn * tiles_m;  // m fastest: neighbouring tiles share a weight panel
     const int n0 = tn * BN, m0 = tm * BM;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wn = wave >> 1, wm = wave & 1;
+    const int wn = wave / WM, wm = wave - wn * WM;
 
-    // staging: instruction g of wave w fills LDS rows q*8 .. q*8+7, q = g*4 + w; lane -> row q*8 + lane/8,
+    // staging: instruction g of wave w fills LDS rows q*8 .. q*8+7, q = g*NW + w; lane -> row q*8 + lane/8,
     // physical chunk lane%8, i.e. logical chunk (lane%8) ^ swz(row).
     const f16* src[GL];
     int lds_off[GL];
 #pragma unroll
     for (int g = 0; g < GL; ++g) {
-        const int q = g * 4 + wave;
+        const int q = g * NW + wave;
         const int row = q * 8 + (lane >> 3);
         const int chunk = (lane & 7) ^ swz(row);
         if (row < BN)
@@ -202,17 +207,28 @@ __global__ __launch_bounds__(256) void gemm_tiled(const f16* __restrict__ X, int
 
     const int KT = K / BK;
     const int fr = lane & 15, fc = lane >> 4;
-    stage(0, 0);
+#pragma unroll
+    for (int s0 = 0; s0 < NST - 1; ++s0)
+        if (s0 < KT) stage(s0, s0);
+    int buf = 0;
     for (int kt = 0; kt < KT; ++kt) {
-        if (kt + 1 < KT) {
-            stage(kt + 1, (kt + 1) & 1);
-            wait_vm<GL>();  // this thread's copies of tile kt have landed
+        // NST - 1 stages ahead: issue tile kt + NST - 1, then wait until tile kt's copies (this thread's) landed
+        const int ahead = KT - 1 - kt;  // tiles after kt
+        if (ahead >= NST - 1) {
+            int nb = buf + NST - 1;
+            nb -= nb >= NST ? NST : 0;
+            stage(kt + NST - 1, nb);
+            wait_vm<GL * (NST - 1)>();
+        } else if (NST >= 4 && ahead == 2) {
+            wait_vm<GL * 2>();
+        } else if (NST >= 3 && ahead == 1) {
+            wait_vm<GL>();
         } else {
             wait_vm<0>();
         }
         __builtin_amdgcn_s_barrier();  // ... and every other wave's
         asm volatile("" ::: "memory");
-        const char* base = smem + (kt & 1) * ROWS * 128;
+        const char* base = smem + buf * ROWS * 128;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = kk * 4 + fc;
@@ -232,7 +248,8 @@ __global__ __launch_bounds__(256) void gemm_tiled(const f16* __restrict__ X, int
 #pragma unroll
                 for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
         }
-        lds_fence_barrier();  // every wave is done reading buffer kt&1 before tile kt+2 is copied into it
+        lds_fence_barrier();  // every wave is done reading this buffer before a later tile is copied into it
+        buf = buf + 1 == NST ? 0 : buf + 1;
     }
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -351,50 +368,88 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
 
 using namespace nsg::lm;
 
+// Tile configurations (ns_lm_gemm_config).  All of them compute every element by the same MFMA chain, so the
+// choice is a speed choice only (tests check equality across configurations bit for bit).
+enum GemmCfg {
+    CFG_DIRECT16 = 0, CFG_DIRECT32, CFG_DIRECT64,     // 16 weight rows x 16/32/64 activation rows per wave
+    CFG_T64_2, CFG_T64_3,                             // 64 x 64 tile, 4 waves, 2 / 3 LDS stages
+    CFG_T128_2, CFG_T128_3, CFG_T128_4,               // 128 x 128, 4 waves (64 x 64 each)
+    CFG_T256x128_2, CFG_T256x128_3,                   // 256 weight rows x 128 activation rows, 8 waves
+    CFG_T128x256_2,                                   // 128 x 256, 8 waves
+    CFG_COUNT
+};
+
 template <int EPI>
-static void launch_gemm(const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y, int64_t ldy,
-                        int M, int N, int K, hipStream_t st) {
-    if (M <= 64) {
-        const dim3 grid((N / 16 + 3) / 4), block(256);
-        if (M <= 16)
-            hipLaunchKernelGGL((gemm_direct<1, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
-        else if (M <= 32)
-            hipLaunchKernelGGL((gemm_direct<2, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
-        else
-            hipLaunchKernelGGL((gemm_direct<4, EPI>), grid, block, 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);
-        return;
-    }
-    const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
-    if (big >= 512) {
-        hipLaunchKernelGGL((gemm_tiled<128, 128, EPI>), dim3((unsigned)big), dim3(256), 0, st, x, ldx, wt, ldw, bias,
-                           y, ldy, M, N, K);
-    } else {
-        const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
-        hipLaunchKernelGGL((gemm_tiled<64, 64, EPI>), dim3((unsigned)tiles), dim3(256), 0, st, x, ldx, wt, ldw, bias,
-                           y, ldy, M, N, K);
+static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y,
+                       int64_t ldy, int M, int N, int K, hipStream_t st) {
+    auto tiles = [&](int bn, int bm) { return dim3((unsigned)(((M + bm - 1) / bm) * (long)((N + bn - 1) / bn))); };
+    switch (cfg) {
+#define NSG_DIRECT(FMv)                                                                                         \
+    hipLaunchKernelGGL((gemm_direct<FMv, EPI>), dim3((N / 16 + 3) / 4, (M + 16 * FMv - 1) / (16 * FMv)),       \
+                       dim3(256), 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K)
+#define NSG_TILED(BNv, BMv, WNv, WMv, NSTv)                                                                    \
+    hipLaunchKernelGGL((gemm_tiled<BNv, BMv, WNv, WMv, NSTv, EPI>), tiles(BNv, BMv), dim3(64 * WNv * WMv), 0, st, \
+                       x, ldx, wt, ldw, bias, y, ldy, M, N, K)
+        case CFG_DIRECT16: NSG_DIRECT(1); break;
+        case CFG_DIRECT32: NSG_DIRECT(2); break;
+        case CFG_DIRECT64: NSG_DIRECT(4); break;
+        case CFG_T64_2: NSG_TILED(64, 64, 2, 2, 2); break;
+        case CFG_T64_3: NSG_TILED(64, 64, 2, 2, 3); break;
+        case CFG_T128_2: NSG_TILED(128, 128, 2, 2, 2); break;
+        case CFG_T128_3: NSG_TILED(128, 128, 2, 2, 3); break;
+        case CFG_T128_4: NSG_TILED(128, 128, 2, 2, 4); break;
+        case CFG_T256x128_2: NSG_TILED(256, 128, 4, 2, 2); break;
+        case CFG_T256x128_3: NSG_TILED(256, 128, 4, 2, 3); break;
+        case CFG_T128x256_2: NSG_TILED(128, 256, 2, 4, 2); break;
+#undef NSG_DIRECT
+#undef NSG_TILED
+        default: break;
     }
 }
 
-extern "C" int ns_lm_gemm(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
-                          int64_t ldy, int M, int N, int K, int epilogue, void* hip_stream) {
+// Automatic choice by shape (speed only: every configuration gives the same bits).
+static int auto_cfg(int M, int N) {
+    if (M <= 16) return CFG_DIRECT16;
+    if (M <= 32) return CFG_DIRECT32;
+    if (M <= 64) return CFG_DIRECT64;
+    const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
+    return big >= 512 ? CFG_T128_2 : CFG_T64_2;
+}
+
+static int gemm_checked(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
+                        int64_t ldy, int M, int N, int K, int epilogue, int cfg, void* hip_stream) {
     if (!d_x || !d_wt || !d_y || M <= 0 || N <= 0 || K <= 0) return NS_ERR_CONFIG;
     if (K % 64 || N % 16) return NS_ERR_UNSUPPORTED;
     if (ldx < K || ldw < K || ldy < N) return NS_ERR_CONFIG;
     const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_wt | (uintptr_t)d_y | (uintptr_t)(d_bias ? d_bias : d_x);
     if ((al & 15u) || (ldx & 7) || (ldw & 7) || (ldy & 3)) return NS_ERR_CONFIG;
-    if ((int64_t)M * ldx > 0x7FFFFFFFFFFFLL || (int64_t)((M + 127) / 128) * ((N + 127) / 128) > 0x7FFFFFFF)
-        return NS_ERR_UNSUPPORTED;
+    if ((int64_t)((M + 15) / 16) * ((N + 15) / 16) > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
+    if (cfg < 0) cfg = auto_cfg(M, N);
+    if (cfg >= CFG_COUNT) return NS_ERR_CONFIG;
     const f16 *x = (const f16*)d_x, *wt = (const f16*)d_wt, *b = (const f16*)d_bias;
     const hipStream_t st = (hipStream_t)hip_stream;
     switch (epilogue) {
-        case NS_LM_EPI_STORE: launch_gemm<NS_LM_EPI_STORE>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
-        case NS_LM_EPI_GELU: launch_gemm<NS_LM_EPI_GELU>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
-        case NS_LM_EPI_RESIDUAL: launch_gemm<NS_LM_EPI_RESIDUAL>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
-        case NS_LM_EPI_STORE_F32: launch_gemm<NS_LM_EPI_STORE_F32>(x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_STORE: launch_cfg<NS_LM_EPI_STORE>(cfg, x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_GELU: launch_cfg<NS_LM_EPI_GELU>(cfg, x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_RESIDUAL: launch_cfg<NS_LM_EPI_RESIDUAL>(cfg, x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
+        case NS_LM_EPI_STORE_F32: launch_cfg<NS_LM_EPI_STORE_F32>(cfg, x, ldx, wt, ldw, b, d_y, ldy, M, N, K, st); break;
         default: return NS_ERR_CONFIG;
     }
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
+
+extern "C" int ns_lm_gemm(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
+                          int64_t ldy, int M, int N, int K, int epilogue, void* hip_stream) {
+    return gemm_checked(d_x, ldx, d_wt, ldw, d_bias, d_y, ldy, M, N, K, epilogue, -1, hip_stream);
+}
+
+extern "C" int ns_lm_gemm_config(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias,
+                                 void* d_y, int64_t ldy, int M, int N, int K, int epilogue, int config,
+                                 void* hip_stream) {
+    return gemm_checked(d_x, ldx, d_wt, ldw, d_bias, d_y, ldy, M, N, K, epilogue, config, hip_stream);
+}
+
+extern "C" int ns_lm_gemm_configs(void) { return CFG_COUNT; }
 
 extern "C" int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
                                int M, int C, float eps, void* hip_stream) {

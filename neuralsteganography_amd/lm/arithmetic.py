@@ -75,7 +75,6 @@ class ByteTokenizer:
 
 
 CTX_CACHE_SIZE = 4  # live coder contexts per provider (distinct quality settings)
-GRAPH_MAX_BATCH = 1024  # auto mode: capture the token step as a hipGraph up to this batch
 
 
 class _StepGraph:
@@ -300,11 +299,11 @@ class HipArithmeticLM:
                      graphs: Optional[bool] = None):
         """Encode B independent bit lists in lockstep (one GPT-2 forward + one coder launch per token).
 
-        With ``graphs`` (and the HIP attention path) the per-token step is captured once as a hipGraph and
-        replayed, which removes the per-launch host cost that dominates at small batch; the cache budget
-        then bounds the replays and the loop continues eagerly (growing the cache) if it runs out.  Default
-        (None): graphs for B <= GRAPH_MAX_BATCH, where launches dominate (at B = 4096 the eager loop measured
-        2 % faster).
+        With ``graphs`` (default; needs the native fp16 step) the per-token step is captured once as a hipGraph
+        and replayed, which removes the per-launch host cost (it dominates at small batch, and at B = 4096 it
+        keeps the GPU busy across the host checks); the cache budget bounds the replays and the loop continues
+        eagerly (growing the cache) if it runs out.  The token history starts at the KV budget: when a stream
+        would outgrow it, the graph is dropped, the history grown and the step captured again.
 
         The reference coder has no underflow handling: when the interval straddles the midpoint and one
         token takes the whole range, no bit is ever fixed and ``code_base/arithmetic.py:114`` loops
@@ -323,11 +322,12 @@ class HipArithmeticLM:
         hard_cap = 64 * max_bits + 4096       # a stream fixing < 1/64 bit per token is reported, not looped
         logits = self.lm.prefill(context, B, budget)
         if graphs is None:
-            graphs = B <= GRAPH_MAX_BATCH
+            graphs = True
         use_graph = graphs and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
-        # token history: a captured graph needs a fixed buffer (the hard cap); the eager loop starts at the
-        # KV budget and grows it at the host checks (at B = 4096 the hard cap alone would be 8.6 GB)
-        sess = EncodeSession(ctx, bit_lists, max_tokens=hard_cap if use_graph else budget, stats=return_stats)
+        # token history: starts at the KV budget and grows at the host checks (a captured graph holds the
+        # buffer's address, so it is re-captured after a growth; the 64x hard cap up front would be 8.6 GB at
+        # B = 4096)
+        sess = EncodeSession(ctx, bit_lists, max_tokens=budget, stats=return_stats)
         stop = _StopCheck(self, sess, stop_text) if stop_text is not None else None
 
         def coder_step(lg):
@@ -347,6 +347,8 @@ class HipArithmeticLM:
                 f = sess.fields()
                 if bool((f["flags"] & 1).all()):
                     break
+                if graph is not None and int(f["ntokens"].max(initial=0)) + check_every + 1 > sess.hist.shape[1]:
+                    logits, graph = graph.logits, None  # the history must grow: re-capture with the new buffer
                 if graph is None:
                     sess.ensure_history(check_every + 1)
                 pos = f["bit_pos"].copy()
@@ -405,7 +407,7 @@ class HipArithmeticLM:
         sess = DecodeSession(ctx, token_lists)
         logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)
         if graphs is None:
-            graphs = B <= GRAPH_MAX_BATCH
+            graphs = True
         if (graphs and sess.T > 2 and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
                 and self.lm.static_capacity_left() >= sess.T):  # replays cannot grow the cache
             graph = _StepGraph(self.lm, sess.step_static, logits)  # runs token 0, captures the next step

@@ -88,6 +88,9 @@ class BatchedGPT2:
         self.head = head
         self.B = 0
         self.L = 0
+        self.T0 = 0  # positions held once in the shared prefix cache (kp, vp) instead of per stream
+        self.position_cap = None  # optional cap on the initial per-stream cache length (the cache still grows)
+        self.kp = self.vp = None
         self.k_cache = self.v_cache = None
         # Decode steps in fp16 on the GPU run entirely on the batch-invariant HIP kernels (include/nsg_lm.h and
         # the fixed-split attention of include/nsg_attn.h; fail loudly if the library is missing): a stream's
@@ -101,8 +104,7 @@ class BatchedGPT2:
         if self.native:
             from .. import _lib
 
-            self._attn = _lib.lib().ns_decode_attention
-            self._attn_dev = _lib.lib().ns_decode_attention_dev
+            self._attn = _lib.lib().ns_decode_attention_prefix
             if self.shape.n_embd // self.shape.n_head != 64:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
             for lw in self.layers:
@@ -120,6 +122,8 @@ class BatchedGPT2:
         """Largest cache length <= ``want`` that fits the device's free memory (keeping ``reserve`` of it for
         activations and logits).  The reference's cache is unbounded; at B = 4096 a 1 KiB payload needs ~1.1k
         positions (170 GB for GPT-2-small fp16), so the budget is sized from what is free, not guessed."""
+        if self.position_cap is not None:
+            want = min(int(want), int(self.position_cap))
         if self.device.type != "cuda":
             return int(want)
         free, _ = torch.cuda.mem_get_info(self.device)
@@ -138,15 +142,19 @@ class BatchedGPT2:
                         "f": torch.empty((B, 4 * C), device=dev, dtype=dt)}
         return self._nb
 
-    def allocate(self, B: int, max_len: int) -> None:
+    def allocate(self, B: int, max_len: int, T0: int = 0) -> None:
+        """Per-stream KV cache for absolute positions [T0, max_len): positions below T0 (the shared context,
+        native path only) live once in ``kp``/``vp`` instead of B times."""
         s = self.shape
         self.k_cache = self.v_cache = None
         hd = s.n_embd // s.n_head
-        shp = (s.n_layer, B, s.n_head, max_len, hd)
+        shp = (s.n_layer, B, s.n_head, max_len - T0, hd)
         # uninitialised: attention only ever reads positions < L + 1, all written before they are read
         self.k_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
         self.v_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
-        self.B, self.L, self.max_len = B, 0, max_len
+        self.B, self.L, self.max_len, self.T0 = B, 0, max_len, T0
+        if T0 == 0:
+            self.kp = self.vp = None
 
     def grow(self, extra: int) -> None:
         """Enlarge the KV cache by ``extra`` positions (copying the filled part); low-entropy streams can
@@ -159,11 +167,12 @@ class BatchedGPT2:
             if new_len <= self.L:
                 raise RuntimeError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
         hd = s.n_embd // s.n_head
-        shp = (s.n_layer, self.B, s.n_head, new_len, hd)
+        T0, n = self.T0, self.L - self.T0  # stream rows filled so far
+        shp = (s.n_layer, self.B, s.n_head, new_len - T0, hd)
         k = torch.empty(shp, device=self.device, dtype=self.dtype)
         v = torch.empty(shp, device=self.device, dtype=self.dtype)
-        k[:, :, :, : self.L] = self.k_cache[:, :, :, : self.L]
-        v[:, :, :, : self.L] = self.v_cache[:, :, :, : self.L]
+        k[:, :, :, :n] = self.k_cache[:, :, :, :n]
+        v[:, :, :, :n] = self.v_cache[:, :, :, :n]
         self.k_cache, self.v_cache, self.max_len = k, v, new_len
 
     def _ln(self, x, wgt, b):
@@ -210,22 +219,31 @@ class BatchedGPT2:
             raise ValueError("context must contain at least one token")
         if min(ctx) < 0 or max(ctx) >= self.shape.vocab:  # host check: never gather out of the table
             raise ValueError(f"context token ids must lie in [0, {self.shape.vocab})")
-        self.allocate(B, self.fit_positions(B, T + max_new))
-        if self.max_len < T + 1:
-            raise RuntimeError(f"no device memory for a {T + 1}-position KV cache at B={B}")
         ids = torch.tensor([ctx], device=self.device, dtype=torch.long)
         pos = torch.arange(T, device=self.device) % self.shape.n_positions
         h = self.wte[ids] + self.wpe[pos][None]
-        # run the context for one stream, then copy its cache to every stream
-        self.B_run = 1
-        saveB = self.B
-        self.B = 1
-        for i in range(self.shape.n_layer):
-            h = self._block(i, h, T, causal=True)
-        self.B = saveB
-        for i in range(self.shape.n_layer):
-            self.k_cache[i, 1:B, :, :T] = self.k_cache[i, 0:1, :, :T]
-            self.v_cache[i, 1:B, :, :T] = self.v_cache[i, 0:1, :, :T]
+        if self.native:
+            # the context's K/V are the same for every stream: keep ONE copy (kp/vp), read by every stream's
+            # attention (ns_decode_attention_prefix) -- B-fold less prefix traffic and memory, identical bits
+            self.allocate(1, T)
+            for i in range(self.shape.n_layer):
+                h = self._block(i, h, T, causal=True)
+            kp, vp = self.k_cache, self.v_cache  # [n_layer, 1, H, T, D]
+            self.allocate(B, T + self.fit_positions(B, max_new), T0=T)
+            self.kp, self.vp = kp, vp
+        else:
+            self.allocate(B, self.fit_positions(B, T + max_new))
+            if self.max_len < T + 1:
+                raise RuntimeError(f"no device memory for a {T + 1}-position KV cache at B={B}")
+            # run the context for one stream, then copy its cache to every stream
+            saveB = self.B
+            self.B = 1
+            for i in range(self.shape.n_layer):
+                h = self._block(i, h, T, causal=True)
+            self.B = saveB
+            for i in range(self.shape.n_layer):
+                self.k_cache[i, 1:B, :, :T] = self.k_cache[i, 0:1, :, :T]
+                self.v_cache[i, 1:B, :, :T] = self.v_cache[i, 0:1, :, :T]
         self.L = T
         lg = self._logits(h[:, -1])
         return lg.expand(B, -1).contiguous()
@@ -275,8 +293,9 @@ class BatchedGPT2:
         if not tok.is_contiguous() or tok.shape != (B,):
             tok = tok.reshape(B).contiguous()
         dL = self.d_L.data_ptr() if dev_len else None
-        if self.L >= self.k_cache.shape[3]:
+        if self.L >= self.max_len:
             raise RuntimeError("KV cache full")  # step() grows the cache before this point
+        T0 = self.T0
         eps = float(s.eps)
 
         def ok(rc, what):
@@ -298,14 +317,13 @@ class BatchedGPT2:
                                      C, B, C, eps, st), "ns_lm_layernorm")
             gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
             kc, vc = self.k_cache[i], self.v_cache[i]
-            if dev_len:
-                rc = self._attn_dev(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
-                                    kc.stride(1), B, H, D, dL, kc.shape[2], o.data_ptr(), o.stride(0),
-                                    1.0 / math.sqrt(D), st)
-            else:
-                rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
-                                kc.stride(1), B, H, D, self.L, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
-            ok(rc, "ns_decode_attention")
+            kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
+            vp = self.vp[i, 0] if T0 else None
+            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+                            kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
+                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, o.data_ptr(),
+                            o.stride(0), 1.0 / math.sqrt(D), st)
+            ok(rc, "ns_decode_attention_prefix")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
             ok(L.ns_lm_layernorm(h.data_ptr(), C, lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), a.data_ptr(), C,
                                  B, C, eps, st), "ns_lm_layernorm")

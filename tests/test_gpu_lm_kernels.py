@@ -116,6 +116,29 @@ def test_gemm_rows_are_batch_invariant(N, K, epi):
         assert torch.equal(y, full[off:off + M]), (M, off)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(1, 768, 768, "store"), (70, 2304, 768, "gelu"), (300, 768, 3072, "residual"),
+                                       (129, 1024, 1024, "f32")])
+def test_gemm_tile_configurations_agree_bitwise(M, N, K, epi):
+    """Every tile configuration (direct 16/32/64-row waves, 64x64 .. 256x128 LDS tiles, 2-4 stages) produces
+    the same bits: the configuration is a speed choice only."""
+    x, wt, bias = _operands(M, N, K, seed=M + 2 * N)
+    ydt = torch.float32 if epi == "f32" else torch.float16
+    y0 = torch.randn((M, N), device="cuda").to(ydt)
+    ref = y0.clone()
+    _gemm(x, wt, bias, ref, epi)
+    n = _lib.lib().ns_lm_gemm_configs()
+    assert n >= 8
+    for cfg in range(n):
+        y = y0.clone()
+        rc = _lib.lib().ns_lm_gemm_config(x.data_ptr(), K, wt.data_ptr(), K, bias.data_ptr(), y.data_ptr(), N, M, N, K,
+                                          EPIS[epi], cfg, _stream_handle())
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), cfg
+    assert _lib.lib().ns_lm_gemm_config(x.data_ptr(), K, wt.data_ptr(), K, None, y0.data_ptr(), N, M, N, K, 0, n,
+                                        None) == _lib.NS_ERR_CONFIG
+
+
 @pytest.mark.parametrize("M,C", [(1, 768), (7, 1024), (300, 768), (5, 64), (33, 1600)])
 def test_layernorm_matches_torch(M, C):
     g = torch.Generator(device="cuda").manual_seed(M + C)
@@ -177,6 +200,43 @@ def test_decode_attention_is_batch_invariant(L0):
                  kc.stride(1), 1, H, D, L0, o1.data_ptr(), o1.stride(0), D ** -0.5, _stream_handle()) == 0
         torch.cuda.synchronize()
         assert torch.equal(o1[0], out[b]), b
+
+
+@pytest.mark.parametrize("T0,L0,dev", [(32, 40, False), (32, 40, True), (1, 1, False), (100, 350, True),
+                                       (7, 7, False)])
+def test_prefix_attention_equals_full_cache(T0, L0, dev):
+    """ns_decode_attention_prefix (context rows stored once, shared by every stream) gives the same bits as
+    ns_decode_attention over a per-stream cache holding the same rows, and appends the new k/v at stream index
+    L0 - T0."""
+    B, H, D = 40, 12, 64
+    cap = L0 + 3
+    g = torch.Generator(device="cuda").manual_seed(T0 + L0)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kp = torch.randn((H, T0, D), generator=g, device="cuda").half()
+    vp = torch.randn((H, T0, D), generator=g, device="cuda").half()
+    ks = torch.randn((B, H, cap - T0, D), generator=g, device="cuda").half()
+    vs = torch.randn((B, H, cap - T0, D), generator=g, device="cuda").half()
+    full_k = torch.cat([kp[None].expand(B, -1, -1, -1), ks], dim=2).contiguous()
+    full_v = torch.cat([vp[None].expand(B, -1, -1, -1), vs], dim=2).contiguous()
+    want = torch.empty((B, H * D), device="cuda").half()
+    lib = _lib.lib()
+    assert lib.ns_decode_attention(qkv.data_ptr(), qkv.stride(0), full_k.data_ptr(), full_v.data_ptr(),
+                                   full_k.stride(0), full_k.stride(1), B, H, D, L0, want.data_ptr(), want.stride(0),
+                                   D ** -0.5, _stream_handle()) == 0
+    got = torch.empty((B, H * D), device="cuda").half()
+    dL = torch.tensor([L0], dtype=torch.int32, device="cuda")
+    assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
+                                          ks.stride(1), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
+                                          -1 if dev else L0, dL.data_ptr() if dev else None, cap, got.data_ptr(),
+                                          got.stride(0), D ** -0.5, _stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    assert torch.equal(ks[:, :, L0 - T0], full_k[:, :, L0]) and torch.equal(vs[:, :, L0 - T0], full_v[:, :, L0])
+    # a position inside the prefix cannot be appended
+    assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
+                                          ks.stride(1), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
+                                          T0 - 1, None, cap, got.data_ptr(), got.stride(0), D ** -0.5,
+                                          None) == _lib.NS_ERR_CONFIG
 
 
 @pytest.mark.parametrize("logits", ["f16", "f32"])

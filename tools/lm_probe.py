@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--model", default="gpt2")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-step", action="store_true")
+    ap.add_argument("--configs", action="store_true", help="time every ns_lm_gemm_config tile configuration")
     args = ap.parse_args()
     import torch
 
@@ -73,8 +74,22 @@ def main():
 
         ms_n, ms_t = timed(native), timed(ref)
         fl = 2.0 * B * N * K
-        print(json.dumps({"gemm": name, "M": B, "N": N, "K": K, "ms_native": ms_n, "ms_torch": ms_t,
-                          "tflops_native": fl / ms_n / 1e9, "tflops_torch": fl / ms_t / 1e9}), flush=True)
+        rec = {"gemm": name, "M": B, "N": N, "K": K, "ms_native": ms_n, "ms_torch": ms_t,
+               "tflops_native": fl / ms_n / 1e9, "tflops_torch": fl / ms_t / 1e9}
+        if args.configs:
+            per = {}
+            for cfg in range(L.ns_lm_gemm_configs()):
+                if cfg < 3 and B > 256:
+                    continue  # direct (small-batch) kernels re-read the weights per 64 rows
+
+                def one(cfg=cfg):
+                    rc = L.ns_lm_gemm_config(xa.data_ptr(), K, wt.data_ptr(), K, bp, y.data_ptr(), N, B, N, K, epi,
+                                             cfg, st)
+                    assert rc == 0
+
+                per[cfg] = round(fl / timed(one) / 1e9, 1)
+            rec["tflops_by_config"] = per
+        print(json.dumps(rec), flush=True)
     a = torch.randn((B, C), device=dev).half()
     ln_out = torch.empty_like(a)
 
