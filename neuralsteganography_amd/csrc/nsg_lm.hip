@@ -5,13 +5,14 @@
 // depend on the batch it runs in: the arithmetic decoder must reproduce the encoder's integer CDF exactly,
 // and a cover encoded among B streams is revealed alone.
 //
-// GEMM: Y[m, n] = epi(sum_k X[m, k] * Wt[n, k] + bias[n]).  Every element is ONE fp32 accumulator chain of
-// v_mfma_f32_16x16x32_f16 over k = 0, 32, 64, ... with the weight row in MFMA row position n & 15 and the
-// activation row in MFMA column position m & 15 -- in every kernel variant.  The variants differ only in how
-// many elements a wave owns and how the operands reach the registers:
-//   * gemm_direct<FM>  (M <= 16 * FM, FM = 1, 2, 4): a wave owns 16 weight rows x 16*FM activation rows and
-//     loads its fragments straight from global memory (the weight row is read once; small batches are
-//     latency- and weight-bandwidth-bound, an LDS round trip would only add latency);
+// GEMM: Y[m, n] = epi(sum_k X[m, k] * Wt[n, k] + bias[n]).  Every element is the in-order sum of SK = 1, 2
+// or 4 (by K only) fp32 accumulator chains of v_mfma_f32_16x16x32_f16 over consecutive k ranges, with the
+// weight row in MFMA row position n & 15 and the activation row in MFMA column position m & 15 -- in every
+// kernel variant.  The variants differ only in how many elements a wave owns and how the operands reach the
+// registers:
+//   * gemm_direct<FM, SK>  (small batches): a wave owns 16 weight rows x 16*FM activation rows x one chain
+//     and loads its fragments straight from global memory (small batches are latency- and weight-bandwidth-
+//     bound, an LDS round trip would only add latency); the chains of one weight block meet in LDS;
 //   * gemm_tiled<BN, BM>: a workgroup of 4 waves owns a BN x BM tile; both operands are staged into LDS with
 //     global_load_lds (16 B per lane, two buffers, counted vmcnt + raw s_barrier so the next K-tile's copy
 //     overlaps this one's MFMAs), rows 128 B long and XOR-swizzled by (row >> 1) & 7 in 16-B chunks so the
@@ -83,18 +84,32 @@ __device__ __forceinline__ void store4(void* Y, int64_t ldy, const f16* __restri
     }
 }
 
+// ------------------------------------------------------------------------------------------ canonical order
+// The K range is cut into SK = chains(K) consecutive chains of 64-wide tiles (SK = 1 up to K = 1024, 2 up to
+// 2048, else 4; tiles_per_chain = ceil(KT / SK)); each chain is ONE fp32 MFMA accumulation from zero, and the
+// chains are added in order, ((c0 + c1) + c2) + c3, before the epilogue.  Every kernel variant follows this
+// order, so the split is part of the result's definition, not of the tile choice -- and it lets a small batch
+// spread a long-K GEMM (GPT-2's mlp c_proj: K = 4C) over SK waves per weight block.
+__host__ __device__ constexpr int k_chains(int K) { return K <= 1024 ? 1 : K <= 2048 ? 2 : 4; }
+
 // ---------------------------------------------------------------------------------------------------- direct
-// 4 waves per workgroup, wave w owns weight rows [16*(4*blockIdx.x + w), +16) and activation rows
-// [16*FM*blockIdx.y, +16*FM).
-template <int FM, int EPI>
+// Workgroup = 4 waves = (4 / SK) weight blocks x SK chains: wave w owns weight rows [16 * nb, +16) with
+// nb = 4 / SK * blockIdx.x + w / SK, activation rows [16 * FM * blockIdx.y, +16 * FM) and chain w % SK; the
+// fragments come straight from global memory (small batches are latency- and weight-bandwidth-bound; an LDS
+// round trip would only add latency).  Chains meet in LDS and the chain-0 wave adds them in order.
+template <int FM, int SK, int EPI>
 __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
                                                    int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
                                                    int M, int N, int K) {
-    const int lane = threadIdx.x & 63;
-    const int nb = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (nb * 16 >= N) return;
+    __shared__ f32x4 s_part[SK > 1 ? 4 : 1][SK > 1 ? FM : 1][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = blockIdx.x * (4 / SK) + wave / SK;
+    const int chain = wave % SK;
+    const bool live = nb * 16 < N;  // uniform per wave; no early return: the chain hand-off has a barrier
     const int m0 = blockIdx.y * 16 * FM;
     const int r = lane & 15, c = lane >> 4;
+    const int KT = K / 64, TPC = (KT + SK - 1) / SK;
+    const int k_begin = min(chain * TPC, KT) * 64, k_end = min((chain + 1) * TPC, KT) * 64;
     const f16* wrow = Wt + (int64_t)min(nb * 16 + r, N - 1) * ldw + c * 8;
     const f16* xrow[FM];
 #pragma unroll
@@ -102,28 +117,39 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
     f32x4 acc[FM];
 #pragma unroll
     for (int f = 0; f < FM; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    constexpr int U = 8;  // 32-wide k-steps per batch of loads (K % 64 == 0 -> K/32 even)
-    int k = 0;
-    for (; k + 32 * U <= K; k += 32 * U) {
-        f16x8 a[U], b[U][FM];
+    constexpr int U = FM == 1 ? 16 : 8;  // 32-wide k-steps per batch of loads in flight
+    int k = k_begin;
+    if (live) {
+        for (; k + 32 * U <= k_end; k += 32 * U) {
+            f16x8 a[U], b[U][FM];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            a[u] = *(const f16x8*)(wrow + k + 32 * u);
+            for (int u = 0; u < U; ++u) {
+                a[u] = *(const f16x8*)(wrow + k + 32 * u);
 #pragma unroll
-            for (int f = 0; f < FM; ++f) b[u][f] = *(const f16x8*)(xrow[f] + k + 32 * u);
+                for (int f = 0; f < FM; ++f) b[u][f] = *(const f16x8*)(xrow[f] + k + 32 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int f = 0; f < FM; ++f) acc[f] = mfma16(a[u], b[u][f], acc[f]);
         }
+        for (; k < k_end; k += 32) {
+            const f16x8 a = *(const f16x8*)(wrow + k);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int f = 0; f < FM; ++f) acc[f] = mfma16(a[u], b[u][f], acc[f]);
+            for (int f = 0; f < FM; ++f) acc[f] = mfma16(a, *(const f16x8*)(xrow[f] + k), acc[f]);
+        }
     }
-    for (; k < K; k += 32) {
-        const f16x8 a = *(const f16x8*)(wrow + k);
+    if constexpr (SK > 1) {
 #pragma unroll
-        for (int f = 0; f < FM; ++f) acc[f] = mfma16(a, *(const f16x8*)(xrow[f] + k), acc[f]);
+        for (int f = 0; f < FM; ++f) s_part[wave][f][lane] = acc[f];
+        __syncthreads();
+        if (chain != 0) return;
+        for (int q = 1; q < SK; ++q)
+#pragma unroll
+            for (int f = 0; f < FM; ++f) acc[f] += s_part[wave + q][f][lane];
     }
     const int n = nb * 16 + 4 * c;
-    if (n >= N) return;
+    if (!live || n >= N) return;
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
         const int m = m0 + f * 16 + r;
@@ -153,7 +179,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
 }
 
-template <int BN, int BM, int WN, int WM, int NST, int EPI>
+template <int BN, int BM, int WN, int WM, int NST, bool SPLIT, int EPI>
 __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict__ X, int64_t ldx,
                                                             const f16* __restrict__ Wt, int64_t ldw,
                                                             const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
@@ -200,12 +226,14 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
     };
 
     f32x4 acc[FN][FM];
+    f32x4 tot[SPLIT ? FN : 1][SPLIT ? FM : 1];  // sum of the finished chains (canonical order)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int KT = K / BK;
+    const int SK = k_chains(K), TPC = (KT + SK - 1) / SK;
     const int fr = lane & 15, fc = lane >> 4;
 #pragma unroll
     for (int s0 = 0; s0 < NST - 1; ++s0)
@@ -228,6 +256,17 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
         }
         __builtin_amdgcn_s_barrier();  // ... and every other wave's
         asm volatile("" ::: "memory");
+        if constexpr (SPLIT) {
+            if (kt > 0 && kt % TPC == 0) {  // a chain ends: fold it into the running total, start the next at 0
+#pragma unroll
+                for (int i = 0; i < FN; ++i)
+#pragma unroll
+                    for (int j = 0; j < FM; ++j) {
+                        tot[i][j] = kt == TPC ? acc[i][j] : tot[i][j] + acc[i][j];
+                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+            }
+        }
         const char* base = smem + buf * ROWS * 128;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -250,6 +289,14 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
         }
         lds_fence_barrier();  // every wave is done reading this buffer before a later tile is copied into it
         buf = buf + 1 == NST ? 0 : buf + 1;
+    }
+    if constexpr (SPLIT) {
+        if (KT > TPC) {
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = tot[i][j] + acc[i][j];
+        }
     }
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -379,17 +426,40 @@ enum GemmCfg {
     CFG_COUNT
 };
 
+template <int FM, int EPI>
+static void launch_direct(const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y,
+                          int64_t ldy, int M, int N, int K, hipStream_t st) {
+    const int nbk = N / 16, my = (M + 16 * FM - 1) / (16 * FM);
+    switch (k_chains(K)) {
+        case 1:
+            hipLaunchKernelGGL((gemm_direct<FM, 1, EPI>), dim3((nbk + 3) / 4, my), dim3(256), 0, st, x, ldx, wt, ldw,
+                               bias, y, ldy, M, N, K);
+            break;
+        case 2:
+            hipLaunchKernelGGL((gemm_direct<FM, 2, EPI>), dim3((nbk + 1) / 2, my), dim3(256), 0, st, x, ldx, wt, ldw,
+                               bias, y, ldy, M, N, K);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_direct<FM, 4, EPI>), dim3(nbk, my), dim3(256), 0, st, x, ldx, wt, ldw, bias, y,
+                               ldy, M, N, K);
+            break;
+    }
+}
+
 template <int EPI>
 static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y,
                        int64_t ldy, int M, int N, int K, hipStream_t st) {
     auto tiles = [&](int bn, int bm) { return dim3((unsigned)(((M + bm - 1) / bm) * (long)((N + bn - 1) / bn))); };
+    const bool split = k_chains(K) > 1;
     switch (cfg) {
-#define NSG_DIRECT(FMv)                                                                                         \
-    hipLaunchKernelGGL((gemm_direct<FMv, EPI>), dim3((N / 16 + 3) / 4, (M + 16 * FMv - 1) / (16 * FMv)),       \
-                       dim3(256), 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K)
-#define NSG_TILED(BNv, BMv, WNv, WMv, NSTv)                                                                    \
-    hipLaunchKernelGGL((gemm_tiled<BNv, BMv, WNv, WMv, NSTv, EPI>), tiles(BNv, BMv), dim3(64 * WNv * WMv), 0, st, \
-                       x, ldx, wt, ldw, bias, y, ldy, M, N, K)
+#define NSG_DIRECT(FMv) launch_direct<FMv, EPI>(x, ldx, wt, ldw, bias, y, ldy, M, N, K, st)
+#define NSG_TILED(BNv, BMv, WNv, WMv, NSTv)                                                                     \
+    if (split)                                                                                                  \
+        hipLaunchKernelGGL((gemm_tiled<BNv, BMv, WNv, WMv, NSTv, true, EPI>), tiles(BNv, BMv), dim3(64 * WNv * WMv), \
+                           0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K);                                      \
+    else                                                                                                        \
+        hipLaunchKernelGGL((gemm_tiled<BNv, BMv, WNv, WMv, NSTv, false, EPI>), tiles(BNv, BMv),                 \
+                           dim3(64 * WNv * WMv), 0, st, x, ldx, wt, ldw, bias, y, ldy, M, N, K)
         case CFG_DIRECT16: NSG_DIRECT(1); break;
         case CFG_DIRECT32: NSG_DIRECT(2); break;
         case CFG_DIRECT64: NSG_DIRECT(4); break;
@@ -407,13 +477,16 @@ static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_
     }
 }
 
-// Automatic choice by shape (speed only: every configuration gives the same bits).
-static int auto_cfg(int M, int N) {
-    if (M <= 16) return CFG_DIRECT16;
-    if (M <= 32) return CFG_DIRECT32;
-    if (M <= 64) return CFG_DIRECT64;
-    const long big = (long)((M + 127) / 128) * ((N + 127) / 128);
-    return big >= 512 ? CFG_T128_2 : CFG_T64_2;
+// Automatic choice by shape (speed only: every configuration gives the same bits).  From the per-config sweep
+// at M = 16 ... 4096 on GPT-2 shapes (profiles/lmprobe_r02j_*.jsonl): 64 x 64 LDS tiles for the short-K GEMMs
+// from M = 16 up; direct waves for the long-K (split) GEMM up to M = 256, where spreading the chains over
+// waves beats tiling; 128 x 128 tiles only for the vocabulary-wide head at large M.
+static int auto_cfg(int M, int N, int K) {
+    const bool split = k_chains(K) > 1;
+    if (M <= 16) return (N >= 8192 && !split) ? CFG_T64_2 : CFG_DIRECT16;
+    if (split && M <= 256) return M <= 64 ? CFG_DIRECT16 : M <= 128 ? CFG_DIRECT32 : CFG_DIRECT64;
+    if (N >= 8192 && M >= 512) return CFG_T128_2;
+    return CFG_T64_2;
 }
 
 static int gemm_checked(const void* d_x, int64_t ldx, const void* d_wt, int64_t ldw, const void* d_bias, void* d_y,
@@ -424,7 +497,7 @@ static int gemm_checked(const void* d_x, int64_t ldx, const void* d_wt, int64_t 
     const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_wt | (uintptr_t)d_y | (uintptr_t)(d_bias ? d_bias : d_x);
     if ((al & 15u) || (ldx & 7) || (ldw & 7) || (ldy & 3)) return NS_ERR_CONFIG;
     if ((int64_t)((M + 15) / 16) * ((N + 15) / 16) > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
-    if (cfg < 0) cfg = auto_cfg(M, N);
+    if (cfg < 0) cfg = auto_cfg(M, N, K);
     if (cfg >= CFG_COUNT) return NS_ERR_CONFIG;
     const f16 *x = (const f16*)d_x, *wt = (const f16*)d_wt, *b = (const f16*)d_bias;
     const hipStream_t st = (hipStream_t)hip_stream;
