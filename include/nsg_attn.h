@@ -43,15 +43,33 @@ int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
 
 /* The general form: positions [0, T0) are a prefix SHARED by all B streams (the common context, stored once:
  * element (h, j, d) at h*prefix_h_stride + j*D + d, j < T0), positions [T0, L0] are the stream's own rows at
- * index j - T0 of d_k_cache / d_v_cache (element (b, h, j - T0, d)).  `cap` = total positions (prefix + the
- * stream cache's rows); the new token is written at stream index L0 - T0.  L0 comes from *d_L0 when d_L0 is not
- * NULL (graph replays), else from the argument.  T0 = 0 is ns_decode_attention(_dev).  The output bits do not
- * depend on where a row is stored (same values, same order). */
+ * index r = j - T0 of d_k_cache / d_v_cache, grouped in 32-row chunks: element (b, h, r, d) at
+ * b*cache_b_stride + h*cache_h_stride + (r/32)*cache_chunk_stride + (r%32)*D + d.  cache_chunk_stride = 0 (or
+ * 32*D) is the plain per-pair row-contiguous layout; a chunk-plane layout (cache_chunk_stride = B*H*32*D,
+ * cache_b_stride = H*32*D, cache_h_stride = 32*D) keeps the rows every step reads dense in memory whatever
+ * the cache's capacity (fewer pages touched).  `cap` = total positions (prefix + the stream cache's rows); the
+ * new token is written at stream index L0 - T0.  L0 comes from *d_L0 when d_L0 is not NULL (graph replays),
+ * else from the argument.  T0 = 0 is ns_decode_attention(_dev).  The output bits do not depend on where a
+ * row is stored (same values, same order). */
 int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
-                               int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
-                               const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
-                               const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
-                               void* hip_stream);
+                               int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
+                               const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B,
+                               int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out, int64_t out_stride,
+                               float scale, void* hip_stream);
+
+/* ns_decode_attention_prefix over an fp8 KV cache (OCP e4m3fn bytes, element layout as above with 1-byte
+ * elements): half the HBM bytes of the fp16 cache.  The new token's k/v are quantised (saturated to +-448,
+ * round to nearest even) before they are stored and used.  q, scores and the softmax stay fp16/fp32; rows
+ * are split by key count only (64-row chunks), so the output is batch-invariant too.  An opt-in numerics
+ * mode: logits differ from the fp16 cache's at the fp8 quantisation level. */
+int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                            int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
+                            const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B,
+                            int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out, int64_t out_stride,
+                            float scale, void* hip_stream);
+
+/* fp16 [n] -> fp8 e4m3fn [n] with the attention's conversion (n % 4 == 0, 8-byte aligned). */
+int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream);
 
 #ifdef __cplusplus
 }

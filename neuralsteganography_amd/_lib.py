@@ -29,6 +29,7 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
+           "ns_decode_attention_fp8", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
            "ns_lm_embed_ln")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
@@ -124,9 +125,13 @@ def lib() -> ctypes.CDLL:
     L.ns_decode_attention.argtypes = [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_float, vp]
     i64, ci = ctypes.c_int64, ctypes.c_int
-    L.ns_decode_attention_prefix.restype = ci
-    L.ns_decode_attention_prefix.argtypes = [vp, i64, vp, vp, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, vp,
-                                             i64, ctypes.c_float, vp]
+    for name in ("ns_decode_attention_prefix", "ns_decode_attention_fp8"):
+        f = getattr(L, name)
+        f.restype = ci
+        f.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, vp, i64, ctypes.c_float,
+                      vp]
+    L.ns_quantize_fp8.restype = ci
+    L.ns_quantize_fp8.argtypes = [vp, vp, i64, vp]
     L.ns_lm_gemm.restype = ci
     L.ns_lm_gemm.argtypes = [vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, ci, vp]
     L.ns_lm_gemm_config.restype = ci

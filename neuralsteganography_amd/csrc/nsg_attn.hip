@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "nsg_attn.h"
 #include "nsg_coder.h"
 
@@ -33,6 +35,7 @@ constexpr int ATT_U = 4;      // 8-row chunks per loop iteration: 32 keys per wa
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float dot8(f16x8 a, f16x8 b) {
     float s = 0.0f;
@@ -56,6 +59,88 @@ __device__ __forceinline__ int att_split(int Lk) {
     return Lk <= NSG_ATT_ROWS1 ? 1 : Lk <= 2 * NSG_ATT_ROWS1 ? 2 : Lk <= 4 * NSG_ATT_ROWS1 ? 4 : 8;
 }
 
+// K/V storage formats.  A lane holds DPL consecutive dims of one key row, LPR lanes a row, RPI rows per 16-byte
+// wave-load, NI wave-loads per 32-row chunk.  The fp16 format is the reference configuration; the fp8 one
+// (OCP e4m3fn, saturated to +-448, round to nearest even; opt-in) halves the cache bytes the HBM-bound decode
+// reads.  q stays fp16 either way; scores and the softmax run in fp32.
+struct FmtF16 {
+    static constexpr int DPL = 8, LPR = 8, RPI = 8, NI = 4;
+    typedef _Float16 Elem;
+    typedef f16x8 Raw;
+    struct Q {
+        f16x8 v;
+    };
+    static __device__ __forceinline__ Q load_q(const _Float16* p) { return Q{*(const f16x8*)p}; }
+    static __device__ __forceinline__ Raw from_qkv(const _Float16* p) { return *(const f16x8*)p; }
+    static __device__ __forceinline__ float dot(const Q& q, Raw k) { return dot8(q.v, k); }
+    static __device__ __forceinline__ void unpack(Raw v, float* f) { unpack8(v, f); }
+};
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+    // saturate first: the conversion itself does not clamp, and e4m3fn has no infinity
+    a = fminf(fmaxf(a, -448.0f), 448.0f);
+    b = fminf(fmaxf(b, -448.0f), 448.0f);
+    c = fminf(fmaxf(c, -448.0f), 448.0f);
+    d = fminf(fmaxf(d, -448.0f), 448.0f);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+    return (uint32_t)w;
+}
+
+#ifndef NSG_ATT_F8_NI
+#define NSG_ATT_F8_NI 2  // 16-row wave-loads per fp8 chunk
+#endif
+
+struct FmtF8 {
+    static constexpr int DPL = 16, LPR = 4, RPI = 16, NI = NSG_ATT_F8_NI;
+    typedef uint8_t Elem;
+    typedef u32x4 Raw;
+    struct Q {
+        f16x8 a, b;  // the lane's 16 query dims, fp16
+    };
+    static __device__ __forceinline__ Q load_q(const _Float16* p) {
+        return Q{*(const f16x8*)p, *(const f16x8*)(p + 8)};
+    }
+    static __device__ __forceinline__ Raw from_qkv(const _Float16* p) {  // the new token's k or v, quantised
+        const f16x8 a = *(const f16x8*)p, b = *(const f16x8*)(p + 8);
+        Raw r;
+        r[0] = pack4_fp8((float)a[0], (float)a[1], (float)a[2], (float)a[3]);
+        r[1] = pack4_fp8((float)a[4], (float)a[5], (float)a[6], (float)a[7]);
+        r[2] = pack4_fp8((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+        r[3] = pack4_fp8((float)b[4], (float)b[5], (float)b[6], (float)b[7]);
+        return r;
+    }
+    // v (fp8, exact in f32) for the PV accumulation: one v_cvt_pk_f32_fp8 per 2 values
+    static __device__ __forceinline__ void unpack(Raw v, float* f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[i], false);
+            const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[i], true);
+            f[4 * i + 0] = lo[0];
+            f[4 * i + 1] = lo[1];
+            f[4 * i + 2] = hi[0];
+            f[4 * i + 3] = hi[1];
+        }
+    }
+    // q.k: every e4m3 value is exact in fp16, so k goes fp8 -> fp16 pairs (v_cvt_scalef32_pk_f16_fp8, scale 1) and
+    // the products run on v_dot2c_f32_f16 like the fp16 cache's, two dims per instruction
+    static __device__ __forceinline__ float dot(const Q& q, Raw k) {
+        const f16x2 qp[8] = {__builtin_shufflevector(q.a, q.a, 0, 1), __builtin_shufflevector(q.a, q.a, 2, 3),
+                             __builtin_shufflevector(q.a, q.a, 4, 5), __builtin_shufflevector(q.a, q.a, 6, 7),
+                             __builtin_shufflevector(q.b, q.b, 0, 1), __builtin_shufflevector(q.b, q.b, 2, 3),
+                             __builtin_shufflevector(q.b, q.b, 4, 5), __builtin_shufflevector(q.b, q.b, 6, 7)};
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8((int)k[i], 1.0f, false);
+            const f16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8((int)k[i], 1.0f, true);
+            s = __builtin_amdgcn_fdot2(lo, qp[2 * i], s, false);
+            s = __builtin_amdgcn_fdot2(hi, qp[2 * i + 1], s, false);
+        }
+        return s;
+    }
+};
+
 // Workgroup = 8 waves serving P consecutive pairs (P = 1 for small batches, 8 otherwise; P changes only which
 // workgroup computes a pair, not how).  With S = att_split(L0 + 1), the waves form 8/S groups of S; group
 // q takes pairs q, q + 8/S, ... of the workgroup, one round per pair, all waves running the same number of
@@ -63,14 +148,17 @@ __device__ __forceinline__ int att_split(int Lk) {
 // Positions [0, T0) come from a prefix shared by every stream (kp/vp, head stride ph: the common context,
 // stored once), positions [T0, L0] from the stream's own cache at index position - T0.  Same values, same
 // order: the output bits do not depend on where a row is stored.
-template <int P>
+template <class F, int P>
 __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __restrict__ qkv, int64_t qkv_stride,
-                                                          _Float16* kc, _Float16* vc, int64_t cb, int64_t ch,
-                                                          const _Float16* __restrict__ kp,
-                                                          const _Float16* __restrict__ vp, int64_t ph, int T0, int B,
-                                                          int H, int L0, const int32_t* __restrict__ L0p, int cap,
-                                                          _Float16* __restrict__ out, int64_t out_stride,
+                                                          typename F::Elem* kc, typename F::Elem* vc, int64_t cb,
+                                                          int64_t ch, int64_t cz, const typename F::Elem* __restrict__ kp,
+                                                          const typename F::Elem* __restrict__ vp, int64_t ph, int T0,
+                                                          int B, int H, int L0, const int32_t* __restrict__ L0p,
+                                                          int cap, _Float16* __restrict__ out, int64_t out_stride,
                                                           float scale_log2) {
+    typedef typename F::Elem E;
+    typedef typename F::Raw Raw;
+    constexpr int DPL = F::DPL, LPR = F::LPR, RPI = F::RPI, NI = F::NI;
     if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
     if (L0 < T0 || L0 >= cap) return;                    // never write past the cache (host checks capacity)
     __shared__ float s_m[8], s_l[8];
@@ -80,8 +168,8 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int grp = wave / S, wv = wave - grp * S, ngrp = 8 / S;
-    const int g = lane >> 3;  // row within an 8-row chunk
-    const int c = lane & 7;   // 8-dim slice
+    const int g = lane / LPR;  // row within an RPI-row slab
+    const int c = lane % LPR;  // DPL-dim slice
     const int C = H * ATT_D;
     const int last_cached = L0 > 0 ? L0 - 1 : 0;
     const int rounds = (P + ngrp - 1) / ngrp;
@@ -90,80 +178,103 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
         const int pair = blockIdx.x * P + j;
         const bool active = j < P && pair < B * H;  // uniform per wave group
         float m = -1e30f, l = 0.0f;
-        float acc[8];
+        float acc[DPL];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+        for (int d = 0; d < DPL; ++d) acc[d] = 0.0f;
         int b = 0, h = 0;
         if (active) {
             b = pair / H;
             h = pair - b * H;
-            const _Float16* qrow = qkv + (int64_t)b * qkv_stride + h * ATT_D + c * 8;
-            const f16x8 q = *(const f16x8*)qrow;
-            const f16x8 knew = *(const f16x8*)(qrow + C);
-            const f16x8 vnew = *(const f16x8*)(qrow + 2 * C);
+            const _Float16* qrow = qkv + (int64_t)b * qkv_stride + h * ATT_D + c * DPL;
+            const typename F::Q q = F::load_q(qrow);
+            const Raw knew = F::from_qkv(qrow + C);
+            const Raw vnew = F::from_qkv(qrow + 2 * C);
             // stream rows are addressed by position (index position - T0 folded into the base)
-            _Float16* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * 8 - (int64_t)T0 * ATT_D;
-            _Float16* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * 8 - (int64_t)T0 * ATT_D;
-            const _Float16* kpb = kp + (int64_t)h * ph + c * 8;
-            const _Float16* vpb = vp + (int64_t)h * ph + c * 8;
+            // stream row j (position T0 + j) at (j / 32) * cz + (j % 32) * D: rows grouped in 32-row chunks, the
+            // chunks of all (stream, head) pairs at one position range side by side (cz = chunk plane stride;
+            // cz = 32 * D is the plain row-contiguous layout)
+            E* kb = kc + (int64_t)b * cb + (int64_t)h * ch + c * DPL;
+            E* vb = vc + (int64_t)b * cb + (int64_t)h * ch + c * DPL;
+            auto soff = [&](int row) -> int64_t {
+                const int jj = row - T0;
+                return (int64_t)(jj >> 5) * cz + (int64_t)(jj & 31) * ATT_D;
+            };
+            const E* kpb = kp + (int64_t)h * ph + c * DPL;
+            const E* vpb = vp + (int64_t)h * ph + c * DPL;
             if (g == 0 && wv == 0) {  // KV append of the new token (position L0)
-                *(f16x8*)(kb + (int64_t)L0 * ATT_D) = knew;
-                *(f16x8*)(vb + (int64_t)L0 * ATT_D) = vnew;
+                *(Raw*)(kb + soff(L0)) = knew;
+                *(Raw*)(vb + soff(L0)) = vnew;
             }
-            for (int j0 = wv * 8 * ATT_U; j0 < Lk; j0 += S * 8 * ATT_U) {
-                f16x8 kr[ATT_U], vr[ATT_U];
+            // one chunk of RPI*NI rows; GENERAL handles the prefix boundary, the clamp past the cache, rows past
+            // Lk and the new token from registers -- an interior chunk (all rows stream rows < L0) skips those
+            // selects (same operations on the same values: the bits do not depend on the path)
+            auto chunk = [&](int j0, auto general) {
+                constexpr bool GEN = decltype(general)::value;
+                Raw kr[NI], vr[NI];
 #pragma unroll
-                for (int u = 0; u < ATT_U; ++u) {
-                    const int row = min(j0 + 8 * u + g, last_cached);
-                    const bool pre = row < T0;
-                    const _Float16* ka = (pre ? kpb : kb) + (int64_t)row * ATT_D;
-                    const _Float16* va = (pre ? vpb : vb) + (int64_t)row * ATT_D;
-                    kr[u] = __builtin_nontemporal_load((const f16x8*)ka);
-                    vr[u] = __builtin_nontemporal_load((const f16x8*)va);
+                for (int u = 0; u < NI; ++u) {
+                    if constexpr (GEN) {
+                        const int row = min(j0 + RPI * u + g, last_cached);
+                        const bool pre = row < T0;
+                        const E* ka = pre ? kpb + (int64_t)row * ATT_D : kb + soff(row);
+                        const E* va = pre ? vpb + (int64_t)row * ATT_D : vb + soff(row);
+                        kr[u] = __builtin_nontemporal_load((const Raw*)ka);
+                        vr[u] = __builtin_nontemporal_load((const Raw*)va);
+                    } else {
+                        const int row = j0 + RPI * u + g;
+                        const int64_t o = soff(row);
+                        kr[u] = __builtin_nontemporal_load((const Raw*)(kb + o));
+                        vr[u] = __builtin_nontemporal_load((const Raw*)(vb + o));
+                    }
                 }
-                float sc[ATT_U];
-                bool valid[ATT_U];
+                float sc[NI];
+                bool valid[NI];
                 float mx = m;
 #pragma unroll
-                for (int u = 0; u < ATT_U; ++u) {
-                    const int row = j0 + 8 * u + g;
-                    valid[u] = row < Lk;
-                    if (row == L0) {  // the new token: from registers, not from the cache just written
+                for (int u = 0; u < NI; ++u) {
+                    const int row = j0 + RPI * u + g;
+                    valid[u] = GEN ? row < Lk : true;
+                    if (GEN && row == L0) {  // the new token: from registers, not from the cache just written
                         kr[u] = knew;
                         vr[u] = vnew;
                     }
-                    float sv = dot8(q, kr[u]);
-                    sv += __shfl_xor(sv, 1);
-                    sv += __shfl_xor(sv, 2);
-                    sv += __shfl_xor(sv, 4);
+                    float sv = F::dot(q, kr[u]);
+#pragma unroll
+                    for (int off = 1; off < LPR; off <<= 1) sv += __shfl_xor(sv, off);
                     sc[u] = sv * scale_log2;
                     if (valid[u]) mx = fmaxf(mx, sc[u]);
                 }
                 const float alpha = exp2f(m - mx);
                 l *= alpha;
 #pragma unroll
-                for (int d = 0; d < 8; ++d) acc[d] *= alpha;
+                for (int d = 0; d < DPL; ++d) acc[d] *= alpha;
 #pragma unroll
-                for (int u = 0; u < ATT_U; ++u) {
+                for (int u = 0; u < NI; ++u) {
                     const float p = valid[u] ? exp2f(sc[u] - mx) : 0.0f;
                     l += p;
-                    float v[8];
-                    unpack8(vr[u], v);
+                    float v[DPL];
+                    F::unpack(vr[u], v);
 #pragma unroll
-                    for (int d = 0; d < 8; ++d) acc[d] = fmaf(p, v[d], acc[d]);
+                    for (int d = 0; d < DPL; ++d) acc[d] = fmaf(p, v[d], acc[d]);
                 }
                 m = mx;
+            };
+            for (int j0 = wv * RPI * NI; j0 < Lk; j0 += S * RPI * NI) {
+                if (j0 >= T0 && j0 + RPI * NI <= L0)  // wave-uniform
+                    chunk(j0, std::false_type{});
+                else
+                    chunk(j0, std::true_type{});
             }
-            // merge the 8 row groups (lanes c, c+8, ..., c+56 hold the same dims)
+            // merge the row groups (lanes c, c + LPR, ... hold the same dims)
 #pragma unroll
-            for (int off = 8; off < 64; off <<= 1) {
+            for (int off = LPR; off < 64; off <<= 1) {
                 const float mo = __shfl_xor(m, off);
                 const float lo = __shfl_xor(l, off);
                 const float mn = fmaxf(m, mo);
                 const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
                 l = l * fa + lo * fo;
 #pragma unroll
-                for (int d = 0; d < 8; ++d) {
+                for (int d = 0; d < DPL; ++d) {
                     const float ao = __shfl_xor(acc[d], off);
                     acc[d] = acc[d] * fa + ao * fo;
                 }
@@ -173,7 +284,7 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
         if (S > 1) {  // uniform over the workgroup: hand the S partials of each group to its first wave
             if (active && g == 0) {
 #pragma unroll
-                for (int d = 0; d < 8; ++d) s_acc[wave][c * 8 + d] = acc[d];
+                for (int d = 0; d < DPL; ++d) s_acc[wave][c * DPL + d] = acc[d];
                 if (c == 0) {
                     s_m[wave] = m;
                     s_l[wave] = l;
@@ -186,46 +297,71 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                 for (int w = 1; w < S; ++w) mt = fmaxf(mt, s_m[w0 + w]);
                 l = 0.0f;
 #pragma unroll
-                for (int d = 0; d < 8; ++d) acc[d] = 0.0f;
+                for (int d = 0; d < DPL; ++d) acc[d] = 0.0f;
                 for (int w = 0; w < S; ++w) {
                     const float f = exp2f(s_m[w0 + w] - mt);
                     l += s_l[w0 + w] * f;
 #pragma unroll
-                    for (int d = 0; d < 8; ++d) acc[d] += s_acc[w0 + w][c * 8 + d] * f;
+                    for (int d = 0; d < DPL; ++d) acc[d] += s_acc[w0 + w][c * DPL + d] * f;
                 }
             }
             __syncthreads();  // the LDS slots are reused by the next round
         }
         if (active && wv == 0 && g == 0) {
             const float inv = 1.0f / l;
-            f16x8 o;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = (_Float16)(acc[i] * inv);
-            *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * 8) = o;
+            for (int h8 = 0; h8 < DPL / 8; ++h8) {
+                f16x8 o;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = (_Float16)(acc[h8 * 8 + i] * inv);
+                *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * DPL + h8 * 8) = o;
+            }
         }
     }
 }
 
+// fp16 -> fp8 (e4m3fn) with the same saturating round-to-nearest-even conversion as the kernel's KV append
+__global__ void quantize_fp8_kernel(const _Float16* __restrict__ src, uint32_t* __restrict__ dst, int64_t n4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const _Float16* s4 = src + 4 * i;
+    dst[i] = pack4_fp8((float)s4[0], (float)s4[1], (float)s4[2], (float)s4[3]);
+}
+
 }  // namespace nsg
 
+template <class F>
 static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
-                            int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
+                            int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
+                            const void* d_k_prefix,
                             const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
                             const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
                             void* hip_stream) {
+    typedef typename F::Elem E;
     if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0 || T0 < 0) return NS_ERR_CONFIG;
     if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
-    if (T0 > 0 && (!d_k_prefix || !d_v_prefix || prefix_h_stride < (int64_t)T0 * D || (prefix_h_stride & 7)))
+    constexpr int ALIGN_E = 16 / (int)sizeof(E);  // elements per 16-byte unit of the cache
+    if (T0 > 0 && (!d_k_prefix || !d_v_prefix || prefix_h_stride < (int64_t)T0 * D || (prefix_h_stride % ALIGN_E)))
         return NS_ERR_CONFIG;
     if (!d_L0 && L0 < T0) return NS_ERR_CONFIG;
     const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_k_cache | (uintptr_t)d_v_cache | (uintptr_t)d_out |
                             (uintptr_t)(T0 > 0 ? d_k_prefix : d_qkv) | (uintptr_t)(T0 > 0 ? d_v_prefix : d_qkv);
-    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || (cache_b_stride & 7) || (cache_h_stride & 7))
+    if (cache_chunk_stride == 0) cache_chunk_stride = 32LL * D;  // plain layout: rows contiguous per (b, h)
+    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || (cache_b_stride % ALIGN_E) ||
+        (cache_h_stride % ALIGN_E) || (cache_chunk_stride % ALIGN_E))
         return NS_ERR_CONFIG;  // 16-byte rows
     if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
-    // the stream cache holds positions [T0, cap): cap - T0 rows per (stream, head)
-    if (cap <= T0 || cache_h_stride < (int64_t)(cap - T0) * D || cache_b_stride < (int64_t)H * cache_h_stride)
-        return NS_ERR_CONFIG;
+    // the stream cache holds positions [T0, cap): cap - T0 rows per (stream, head), in 32-row chunks
+    if (cap <= T0) return NS_ERR_CONFIG;
+    const int64_t nchunks = (cap - T0 + 31) / 32;
+    if (cache_chunk_stride == 32LL * D && cache_h_stride >= (int64_t)(cap - T0) * D) {
+        // plain: a pair's rows contiguous, pairs apart by the h / b strides
+        if (cache_b_stride < (int64_t)H * cache_h_stride) return NS_ERR_CONFIG;
+    } else {  // chunked: a plane of B*H chunks per 32 positions
+        if (cache_h_stride < 32LL * D || cache_b_stride < (int64_t)H * cache_h_stride ||
+            cache_chunk_stride < (int64_t)B * cache_b_stride || nchunks < 1)
+            return NS_ERR_CONFIG;
+    }
     if (!d_L0 && L0 >= cap) return NS_ERR_CONFIG;
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     const int pairs = B * H;
@@ -235,25 +371,27 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     // decoded alone).  Pairs per workgroup follow the batch: 8 when there are enough pairs to fill the chip.
     const hipStream_t st = (hipStream_t)hip_stream;
     const _Float16* q = (const _Float16*)d_qkv;
-    _Float16 *k = (_Float16*)d_k_cache, *v = (_Float16*)d_v_cache, *o = (_Float16*)d_out;
-    const _Float16* kp = T0 > 0 ? (const _Float16*)d_k_prefix : k;
-    const _Float16* vp = T0 > 0 ? (const _Float16*)d_v_prefix : v;
+    E *k = (E*)d_k_cache, *v = (E*)d_v_cache;
+    _Float16* o = (_Float16*)d_out;
+    const E* kp = T0 > 0 ? (const E*)d_k_prefix : k;
+    const E* vp = T0 > 0 ? (const E*)d_v_prefix : v;
     if (pairs <= NSG_ATT_SMALL_PAIRS)
-        hipLaunchKernelGGL(nsg::decode_attn_kernel<1>, dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, kp, vp, prefix_h_stride, T0, B, H, L0, d_L0, cap, o,
-                           out_stride, scale_log2);
+        hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 1>), dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
+                           cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B, H,
+                           L0, d_L0, cap, o, out_stride, scale_log2);
     else
-        hipLaunchKernelGGL(nsg::decode_attn_kernel<8>, dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k, v,
-                           cache_b_stride, cache_h_stride, kp, vp, prefix_h_stride, T0, B, H, L0, d_L0, cap, o,
-                           out_stride, scale_log2);
+        hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 8>), dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k,
+                           v, cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B,
+                           H, L0, d_L0, cap, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
 extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                                    int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
                                    void* d_out, int64_t out_stride, float scale, void* hip_stream) {
-    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, nullptr, nullptr,
-                            0, 0, B, H, D, L0, nullptr, L0 + 1, d_out, out_stride, scale, hip_stream);
+    return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, 0,
+                                         nullptr, nullptr, 0, 0, B, H, D, L0, nullptr, L0 + 1, d_out, out_stride,
+                                         scale, hip_stream);
 }
 
 extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
@@ -261,16 +399,36 @@ extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, vo
                                        const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
                                        void* hip_stream) {
     if (!d_L0 || cap < 1) return NS_ERR_CONFIG;
-    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, nullptr, nullptr,
-                            0, 0, B, H, D, 0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+    return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, 0,
+                                         nullptr, nullptr, 0, 0, B, H, D, 0, d_L0, cap, d_out, out_stride, scale,
+                                         hip_stream);
 }
 
 extern "C" int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
-                                          int64_t cache_b_stride, int64_t cache_h_stride, const void* d_k_prefix,
-                                          const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H,
-                                          int D, int L0, const int32_t* d_L0, int cap, void* d_out,
-                                          int64_t out_stride, float scale, void* hip_stream) {
-    return decode_attention(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, d_k_prefix,
-                            d_v_prefix, prefix_h_stride, T0, B, H, D, d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride,
-                            scale, hip_stream);
+                                          int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
+                                          const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride,
+                                          int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap,
+                                          void* d_out, int64_t out_stride, float scale, void* hip_stream) {
+    return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
+                                         cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
+                                         d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+}
+
+extern "C" int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
+                                       int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
+                                       const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride,
+                                       int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out,
+                                       int64_t out_stride, float scale, void* hip_stream) {
+    return decode_attention<nsg::FmtF8>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
+                                        cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
+                                        d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+}
+
+extern "C" int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream) {
+    if (!d_src || !d_dst || n < 0 || (n & 3) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 7u)) return NS_ERR_CONFIG;
+    if (n == 0) return NS_OK;
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(nsg::quantize_fp8_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)hip_stream, (const _Float16*)d_src, (uint32_t*)d_dst, n4);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }

@@ -36,6 +36,9 @@
 #include "nsg_host.h"
 #include "nsg_host.h"
 
+#ifndef NSG_SAMPLE
+#define NSG_SAMPLE 16  // stratified sample: this many 64-id blocks (values per lane) for the speculative threshold
+#endif
 #ifndef NSG_BUCKET_CAP
 #define NSG_BUCKET_CAP 48  // largest bucket the bucket rank accepts (its fix-up loop runs that often)
 #endif
@@ -563,13 +566,14 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     float r = 0.0f;
     bool spec = false;
     if (p.spec_j > 0) {
-        constexpr int LPB = WAVE / W;  // lanes per 64-id block
-        constexpr int NLD = 16 / W;    // sample loads per lane
-        float sv[16];
+        constexpr int NS = NSG_SAMPLE;  // sample values per lane = 64-id blocks
+        constexpr int LPB = WAVE / W;   // lanes per 64-id block
+        constexpr int NLD = NS / W;     // sample loads per lane
+        float sv[NS];
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int blk = i * W + lane / LPB;
-            const int jb = ((int)(((int64_t)blk * V) / 16) / W) * W + (lane % LPB) * W;
+            const int jb = ((int)(((int64_t)blk * V) / NS) / W) * W + (lane % LPB) * W;
             float x[W];
             Elem<T>::unpack(rd.vec(jb / W), x);
 #pragma unroll
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         }
         float mx = sv[0];
 #pragma unroll
-        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, sv[i]);
+        for (int i = 1; i < NS; ++i) mx = fmaxf(mx, sv[i]);
         r = wave_max(mx);
         if (r == -__builtin_inff()) r = 0.0f;
         uint32_t pre = 0;
@@ -585,7 +589,7 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
             const uint32_t c = pre | (1u << bit);
             int n = 0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) n += popc64(ballot(ord32(sv[i]) >= c));
+            for (int i = 0; i < NS; ++i) n += popc64(ballot(ord32(sv[i]) >= c));
             if (n >= p.spec_j) pre = c;
         }
         if (pre > 0x00800000u) {  // above ord(-inf): a finite threshold
@@ -1240,8 +1244,8 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     p.nbanned = nb;
     for (int i = 0; i < nb; ++i) p.banned[i] = ban[i];
     p.flags = flags;
-    // speculative candidate threshold: the spec_j-th largest of a 1024-id stratified sample.  The number of
-    // sample ids above the row's true K-th key is ~Poisson(lambda = 1024 K / nvalid); spec_j is the smallest j
+    // speculative candidate threshold: the spec_j-th largest of a 64*NSG_SAMPLE-id stratified sample.  The number
+    // of sample ids above the row's true K-th key is ~Poisson(lambda = 64*NSG_SAMPLE*K / nvalid); spec_j is the smallest j
     // with P(Poisson(lambda) >= j) <= 1e-6, so a miss (one extra row read by that wave) stays a rare event
     // for every K.  NSG_SPEC_FACTOR (tuning override) instead sets spec_j = factor * lambda + 1.
     p.spec_j = 0;
@@ -1250,7 +1254,7 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
         return e ? atof(e) : 0.0;
     }();
     if (ctx->vocab >= 2048) {
-        const double lambda = (double)K * 1024.0 / (double)nvalid;
+        const double lambda = (double)K * (64.0 * NSG_SAMPLE) / (double)nvalid;
         int sj;
         if (spec_factor > 0.0) {
             sj = (int)(spec_factor * lambda) + 1;

@@ -156,7 +156,8 @@ class HipArithmeticLM:
     decodes_without_state = True  # the interval coder needs no per-token history (unlike the rank coder)
 
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
-                 compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096):
+                 compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096,
+                 kv_dtype: str = "fp16"):
         import torch
 
         from .gpt2 import BatchedGPT2
@@ -167,7 +168,7 @@ class HipArithmeticLM:
             raise NativeLibraryError("HipArithmeticLM needs a ROCm GPU (the coder has no CPU path)")
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         ldt = torch.float16 if logits_dtype == "f16" else torch.float32
-        lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
+        lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt, kv_dtype=kv_dtype)
         self._init(lm, tokenizer, dev, logits_dtype, banned, max_batch)
 
     @classmethod

@@ -50,7 +50,7 @@ class BatchedGPT2:
     ``compute_dtype`` is the weight/activation dtype (fp16 on the GPU by default); ``logits_dtype`` is what
     the coder reads (``torch.float32`` or ``torch.float16``)."""
 
-    def __init__(self, hf_model, *, device=None, compute_dtype=None, logits_dtype=torch.float32):
+    def __init__(self, hf_model, *, device=None, compute_dtype=None, logits_dtype=torch.float32, kv_dtype="fp16"):
         cfg = hf_model.config
         self.shape = GPT2Shape(cfg.n_layer, cfg.n_head, cfg.n_embd, cfg.vocab_size, cfg.n_positions,
                                cfg.layer_norm_epsilon)
@@ -90,6 +90,7 @@ class BatchedGPT2:
         self.L = 0
         self.T0 = 0  # positions held once in the shared prefix cache (kp, vp) instead of per stream
         self.position_cap = None  # optional cap on the initial per-stream cache length (the cache still grows)
+        self.chunked_cache = True  # native decode: chunk-plane KV layout (False: plain per-pair rows; A/B only)
         self.kp = self.vp = None
         self.k_cache = self.v_cache = None
         # Decode steps in fp16 on the GPU run entirely on the batch-invariant HIP kernels (include/nsg_lm.h and
@@ -99,12 +100,22 @@ class BatchedGPT2:
         # path (SDPA), the forward's reference configuration in the tests.
         self.native = self.device.type == "cuda" and self.dtype == torch.float16
         self.hip_attention = self.native  # graph capture needs the native step (kept name: callers probe it)
+        # KV cache element type: "fp16" (the reference configuration) or "fp8" (OCP e4m3fn, opt-in: half the
+        # bytes the HBM-bound decode attention reads; logits differ at the fp8 quantisation level, the same for
+        # encoder and decoder, batch-invariant)
+        if kv_dtype not in ("fp16", "fp8"):
+            raise ValueError("kv_dtype must be 'fp16' or 'fp8'")
+        if kv_dtype == "fp8" and not self.native:
+            raise ValueError("an fp8 KV cache needs the native fp16 decode step on the GPU")
+        self.kv_dtype = kv_dtype
+        self.kv_torch_dtype = torch.uint8 if kv_dtype == "fp8" else self.dtype
         self.d_L = None
         self._static_logits = None
         if self.native:
             from .. import _lib
 
-            self._attn = _lib.lib().ns_decode_attention_prefix
+            self._attn = (_lib.lib().ns_decode_attention_fp8 if kv_dtype == "fp8"
+                          else _lib.lib().ns_decode_attention_prefix)
             if self.shape.n_embd // self.shape.n_head != 64:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
             for lw in self.layers:
@@ -116,7 +127,7 @@ class BatchedGPT2:
     # ------------------------------------------------------------------
     def kv_bytes_per_position(self, B: int) -> int:
         s = self.shape
-        return 2 * s.n_layer * B * s.n_embd * torch.tensor([], dtype=self.dtype).element_size()
+        return 2 * s.n_layer * B * s.n_embd * torch.tensor([], dtype=self.kv_torch_dtype).element_size()
 
     def fit_positions(self, B: int, want: int, reserve: float = 0.15) -> int:
         """Largest cache length <= ``want`` that fits the device's free memory (keeping ``reserve`` of it for
@@ -127,6 +138,8 @@ class BatchedGPT2:
         if self.device.type != "cuda":
             return int(want)
         free, _ = torch.cuda.mem_get_info(self.device)
+        # memory PyTorch's caching allocator holds but no tensor uses (e.g. a previous call's KV cache) is free too
+        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         if self.k_cache is not None:
             free += 2 * self.k_cache.numel() * self.k_cache.element_size()
         return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
@@ -142,16 +155,34 @@ class BatchedGPT2:
                         "f": torch.empty((B, 4 * C), device=dev, dtype=dt)}
         return self._nb
 
-    def allocate(self, B: int, max_len: int, T0: int = 0) -> None:
-        """Per-stream KV cache for absolute positions [T0, max_len): positions below T0 (the shared context,
-        native path only) live once in ``kp``/``vp`` instead of B times."""
+    def _cache_shape(self, B: int, rows: int, plain: bool):
         s = self.shape
-        self.k_cache = self.v_cache = None
         hd = s.n_embd // s.n_head
-        shp = (s.n_layer, B, s.n_head, max_len - T0, hd)
+        if plain:
+            return (s.n_layer, B, s.n_head, rows, hd)
+        # chunk planes: [layer][rows/32][B][H][32][D] -- the rows a decode step reads stay dense in memory
+        # whatever the capacity (fewer pages touched than per-pair row ranges padded to the capacity)
+        return (s.n_layer, (rows + 31) // 32, B, s.n_head, 32, hd)
+
+    def _cache_strides(self, layer: int):
+        """(b, h, chunk) element strides of one layer's stream cache for the attention kernels."""
+        kc = self.k_cache[layer]
+        if kc.dim() == 5:  # chunk planes [nch, B, H, 32, D]
+            return kc.stride(1), kc.stride(2), kc.stride(0)
+        return kc.stride(0), kc.stride(1), 0  # plain [B, H, rows, D]
+
+    def allocate(self, B: int, max_len: int, T0: int = 0, dtype=None, plain=None) -> None:
+        """Per-stream KV cache for absolute positions [T0, max_len): positions below T0 (the shared context,
+        native path only) live once in ``kp``/``vp`` instead of B times.  The native decode step keeps the cache
+        in chunk planes (``plain`` False); the PyTorch path (and the prefill) in plain [B, H, rows, D] rows."""
+        self.k_cache = self.v_cache = None
+        if plain is None:
+            plain = not self.native or not self.chunked_cache
+        shp = self._cache_shape(B, max_len - T0, plain)
         # uninitialised: attention only ever reads positions < L + 1, all written before they are read
-        self.k_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
-        self.v_cache = torch.empty(shp, device=self.device, dtype=self.dtype)
+        kdt = self.kv_torch_dtype if dtype is None else dtype
+        self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
+        self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
         self.B, self.L, self.max_len, self.T0 = B, 0, max_len, T0
         if T0 == 0:
             self.kp = self.vp = None
@@ -166,13 +197,18 @@ class BatchedGPT2:
             new_len = min(new_len, self.max_len + int(free * 0.9) // (2 * self.kv_bytes_per_position(self.B)))
             if new_len <= self.L:
                 raise RuntimeError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
-        hd = s.n_embd // s.n_head
         T0, n = self.T0, self.L - self.T0  # stream rows filled so far
-        shp = (s.n_layer, self.B, s.n_head, new_len - T0, hd)
-        k = torch.empty(shp, device=self.device, dtype=self.dtype)
-        v = torch.empty(shp, device=self.device, dtype=self.dtype)
-        k[:, :, :, :n] = self.k_cache[:, :, :, :n]
-        v[:, :, :, :n] = self.v_cache[:, :, :, :n]
+        plain = self.k_cache.dim() == 5
+        shp = self._cache_shape(self.B, new_len - T0, plain)
+        k = torch.empty(shp, device=self.device, dtype=self.k_cache.dtype)
+        v = torch.empty(shp, device=self.device, dtype=self.v_cache.dtype)
+        if plain:
+            k[:, :, :, :n] = self.k_cache[:, :, :, :n]
+            v[:, :, :, :n] = self.v_cache[:, :, :, :n]
+        else:
+            nch = (n + 31) // 32  # whole chunk planes: the rows beyond n are never read before written
+            k[:, :nch] = self.k_cache[:, :nch]
+            v[:, :nch] = self.v_cache[:, :nch]
         self.k_cache, self.v_cache, self.max_len = k, v, new_len
 
     def _ln(self, x, wgt, b):
@@ -209,6 +245,19 @@ class BatchedGPT2:
         out = hf @ self.head
         return out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
 
+    def _quantize_fp8(self, t: torch.Tensor) -> torch.Tensor:
+        from .. import _lib
+        from ..coder import _stream_handle
+
+        src = t.contiguous()
+        out = torch.empty(src.shape, device=src.device, dtype=torch.uint8)
+        if src.numel() % 4:
+            raise ValueError("fp8 quantisation needs a multiple of 4 elements")
+        rc = _lib.lib().ns_quantize_fp8(src.data_ptr(), out.data_ptr(), src.numel(), _stream_handle())
+        if rc != 0:
+            raise RuntimeError(f"ns_quantize_fp8 failed ({rc})")
+        return out
+
     @torch.no_grad()
     def prefill(self, context: Sequence[int], B: int, max_new: int) -> torch.Tensor:
         """Run the shared context once (reference: first call, default positions) and broadcast its cache
@@ -225,10 +274,12 @@ class BatchedGPT2:
         if self.native:
             # the context's K/V are the same for every stream: keep ONE copy (kp/vp), read by every stream's
             # attention (ns_decode_attention_prefix) -- B-fold less prefix traffic and memory, identical bits
-            self.allocate(1, T)
+            self.allocate(1, T, dtype=self.dtype, plain=True)  # the prefill itself runs in fp16 (PyTorch path)
             for i in range(self.shape.n_layer):
                 h = self._block(i, h, T, causal=True)
             kp, vp = self.k_cache, self.v_cache  # [n_layer, 1, H, T, D]
+            if self.kv_dtype == "fp8":  # the context rows get the same conversion as the decode-time appends
+                kp, vp = self._quantize_fp8(kp), self._quantize_fp8(vp)
             self.allocate(B, T + self.fit_positions(B, max_new), T0=T)
             self.kp, self.vp = kp, vp
         else:
@@ -307,6 +358,7 @@ class BatchedGPT2:
                             bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), B, N, K, epi,
                             st), "ns_lm_gemm")
 
+        strides = [self._cache_strides(i) for i in range(s.n_layer)]
         lw0 = self.layers[0]
         ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
                             self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
@@ -317,9 +369,10 @@ class BatchedGPT2:
                                      C, B, C, eps, st), "ns_lm_layernorm")
             gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
             kc, vc = self.k_cache[i], self.v_cache[i]
+            sb, sh, sz = strides[i]
             kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
             vp = self.vp[i, 0] if T0 else None
-            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz,
                             kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
                             kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, o.data_ptr(),
                             o.stride(0), 1.0 / math.sqrt(D), st)

@@ -226,7 +226,7 @@ def test_prefix_attention_equals_full_cache(T0, L0, dev):
     got = torch.empty((B, H * D), device="cuda").half()
     dL = torch.tensor([L0], dtype=torch.int32, device="cuda")
     assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
-                                          ks.stride(1), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
+                                          ks.stride(1), 0, kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
                                           -1 if dev else L0, dL.data_ptr() if dev else None, cap, got.data_ptr(),
                                           got.stride(0), D ** -0.5, _stream_handle()) == 0
     torch.cuda.synchronize()
@@ -234,9 +234,47 @@ def test_prefix_attention_equals_full_cache(T0, L0, dev):
     assert torch.equal(ks[:, :, L0 - T0], full_k[:, :, L0]) and torch.equal(vs[:, :, L0 - T0], full_v[:, :, L0])
     # a position inside the prefix cannot be appended
     assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
-                                          ks.stride(1), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
+                                          ks.stride(1), 0, kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
                                           T0 - 1, None, cap, got.data_ptr(), got.stride(0), D ** -0.5,
                                           None) == _lib.NS_ERR_CONFIG
+
+
+@pytest.mark.parametrize("kv", ["fp16", "fp8"])
+@pytest.mark.parametrize("T0,L0", [(0, 100), (32, 32), (32, 300), (5, 1000)])
+def test_chunk_plane_layout_equals_plain(kv, T0, L0):
+    """The chunk-plane cache layout ([chunk][B][H][32][D]: the rows a step reads stay dense whatever the
+    capacity) gives the same bits as the plain [B][H][rows][D] layout holding the same rows, and appends the
+    new token at the same logical position."""
+    B, H, D = 24, 12, 64
+    rows = L0 - T0 + 5
+    nch = (rows + 31) // 32
+    g = torch.Generator(device="cuda").manual_seed(L0 + T0)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    plain_k = torch.randn((B, H, nch * 32, D), generator=g, device="cuda").half()
+    plain_v = torch.randn((B, H, nch * 32, D), generator=g, device="cuda").half()
+    kp = torch.randn((H, max(T0, 1), D), generator=g, device="cuda").half()
+    vp = torch.randn((H, max(T0, 1), D), generator=g, device="cuda").half()
+    if kv == "fp8":
+        plain_k, plain_v, kp, vp = _q8(plain_k), _q8(plain_v), _q8(kp), _q8(vp)
+        f = _lib.lib().ns_decode_attention_fp8
+    else:
+        f = _lib.lib().ns_decode_attention_prefix
+    chunk_k = plain_k.view(B, H, nch, 32, D).permute(2, 0, 1, 3, 4).contiguous()  # [nch, B, H, 32, D]
+    chunk_v = plain_v.view(B, H, nch, 32, D).permute(2, 0, 1, 3, 4).contiguous()
+    cap = T0 + rows
+    outs = []
+    for k, v, strides in ((plain_k, plain_v, (plain_k.stride(0), plain_k.stride(1), 0)),
+                          (chunk_k, chunk_v, (chunk_k.stride(1), chunk_k.stride(2), chunk_k.stride(0)))):
+        o = torch.empty((B, H * D), device="cuda").half()
+        assert f(qkv.data_ptr(), qkv.stride(0), k.data_ptr(), v.data_ptr(), *strides, kp.data_ptr() if T0 else None,
+                 vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D, L0, None, cap, o.data_ptr(),
+                 o.stride(0), D ** -0.5, _stream_handle()) == 0
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    r = L0 - T0
+    assert torch.equal(chunk_k[r // 32, :, :, r % 32], plain_k[:, :, r]) and torch.equal(
+        chunk_v[r // 32, :, :, r % 32], plain_v[:, :, r])
 
 
 @pytest.mark.parametrize("logits", ["f16", "f32"])
@@ -277,6 +315,116 @@ def test_fp16_cover_batch_reveals_alone():
     assert lm.lm.native
     q = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": False}
     secrets = [b"first secret", bytes(range(60)), b"z", b"another one, a little longer than the rest"]
+    seed = "w5. w6. w3"
+    texts = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="none", lm=lm, quality_gate=False,
+                                 chunk_bytes=24)
+    for text, secret in zip(texts, secrets):
+        assert cover_reveal(text, seed_text=seed, quality=q, ecc="none", lm=lm) == secret
+
+
+# ------------------------------------------------------------------------------------------ fp8 KV cache (opt-in)
+def _q8(t):
+    out = torch.empty(t.shape, dtype=torch.uint8, device="cuda")
+    assert _lib.lib().ns_quantize_fp8(t.contiguous().data_ptr(), out.data_ptr(), t.numel(), _stream_handle()) == 0
+    return out
+
+
+def _dq8(u):
+    return u.view(torch.float8_e4m3fn).float()
+
+
+def test_fp8_quantizer_matches_torch_e4m3fn():
+    """ns_quantize_fp8 = round-to-nearest-even OCP e4m3fn with saturation to +-448 (torch's float8_e4m3fn cast
+    of the clamped value)."""
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.cat([torch.randn(4096, generator=g, device="cuda") * s for s in (1e-3, 0.1, 1.0, 30.0, 600.0)]).half()
+    got = _q8(x)
+    want = x.float().clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("B,L0,T0", [(3, 0, 0), (5, 77, 0), (40, 300, 32), (700, 1030, 32), (2, 2000, 1)])
+def test_fp8_attention_matches_fp32_reference(B, L0, T0):
+    """ns_decode_attention_fp8 vs softmax(q k^T / sqrt(D)) v in fp32 over the DEQUANTISED fp8 rows (the new
+    token's k/v quantised the same way); the new k/v land in the cache as fp8.  2e-3 absolute (fp16 output)."""
+    H, D = 12, 64
+    cap = L0 + 4
+    g = torch.Generator(device="cuda").manual_seed(L0 + B)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kf = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    vf = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    k8, v8 = _q8(kf), _q8(vf)
+    kp, vp = k8[0, :, :T0].contiguous(), v8[0, :, :T0].contiguous()
+    ks, vs = k8[:, :, T0:].contiguous(), v8[:, :, T0:].contiguous()
+    out = torch.empty((B, H * D), device="cuda").half()
+    rc = _lib.lib().ns_decode_attention_fp8(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
+                                            ks.stride(1), 0, kp.data_ptr() if T0 else None,
+                                            vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D, L0,
+                                            None, cap, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    q, k, v = qkv.view(B, 3, H, D).unbind(1)
+    kk = torch.cat([kp[None].expand(B, -1, -1, -1), ks], dim=2) if T0 else ks.clone()
+    vv = torch.cat([vp[None].expand(B, -1, -1, -1), vs], dim=2) if T0 else vs.clone()
+    kk, vv = _dq8(kk.contiguous()), _dq8(vv.contiguous())
+    kk[:, :, L0] = _dq8(_q8(k))
+    vv[:, :, L0] = _dq8(_q8(v))
+    s = torch.einsum("bhd,bhjd->bhj", q.float(), kk[:, :, : L0 + 1]) * D ** -0.5
+    want = torch.einsum("bhj,bhjd->bhd", torch.softmax(s, -1), vv[:, :, : L0 + 1]).reshape(B, H * D)
+    assert (out.float() - want).abs().max().item() < 2e-3
+    assert torch.equal(ks[:, :, L0 - T0], _q8(k)) and torch.equal(vs[:, :, L0 - T0], _q8(v))
+
+
+def test_fp8_attention_is_batch_invariant():
+    B, H, D, L0 = 300, 12, 64, 700
+    g = torch.Generator(device="cuda").manual_seed(2)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kc = _q8(torch.randn((B, H, L0 + 2, D), generator=g, device="cuda").half())
+    vc = _q8(torch.randn((B, H, L0 + 2, D), generator=g, device="cuda").half())
+    f = _lib.lib().ns_decode_attention_fp8
+    out = torch.empty((B, H * D), device="cuda").half()
+    assert f(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), 0, None, None,
+             0, 0, B, H, D, L0, None, L0 + 2, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle()) == 0
+    for b in (0, 150, 299):
+        o1 = torch.empty((1, H * D), device="cuda").half()
+        assert f(qkv[b:].data_ptr(), qkv.stride(0), kc[b:].data_ptr(), vc[b:].data_ptr(), kc.stride(0), kc.stride(1),
+                 0, None, None, 0, 0, 1, H, D, L0, None, L0 + 2, o1.data_ptr(), o1.stride(0), D ** -0.5,
+                 _stream_handle()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o1[0], out[b]), b
+
+
+def test_gpt2_fp8_kv_logits_close_and_batch_invariant():
+    """GPT-2-small with the fp8 KV cache: logits within the fp8 quantisation error of the fp16 cache's
+    (random-init weights), and bit-identical for a stream at B = 1 and B = 9."""
+    from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+
+    m = random_gpt2("gpt2", seed=8)
+    ctx = synthetic.DEFAULT_CONTEXT
+    toks = torch.randint(0, 50257, (5, 9), generator=torch.Generator().manual_seed(3))
+    outs = {}
+    for kvd, B in (("fp16", 9), ("fp8", 9), ("fp8", 1)):
+        lm = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16, logits_dtype=torch.float32, kv_dtype=kvd)
+        lo = [lm.prefill(ctx, B, 8)]
+        for t in range(5):
+            lo.append(lm.step(toks[t, :B].cuda()))
+        outs[(kvd, B)] = lo
+    for t in range(6):
+        assert torch.equal(outs[("fp8", 1)][t][0], outs[("fp8", 9)][t][0]), t
+        assert (outs[("fp8", 9)][t] - outs[("fp16", 9)][t]).abs().max().item() < 0.1
+
+
+def test_fp8_kv_cover_batch_reveals_alone():
+    from neuralsteganography_amd.cover import cover_generate_batch, cover_reveal
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from test_gpu_guard import IdTokenizer
+
+    m = random_gpt2("tiny", vocab_size=2000, n_positions=1024, n_embd=128, n_head=2, seed=29)
+    lm = HipArithmeticLM(m, IdTokenizer(2000), compute_dtype=torch.float16, logits_dtype="f16", kv_dtype="fp8")
+    q = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": False}
+    secrets = [b"fp8 cache", bytes(range(40)), b"x"]
     seed = "w5. w6. w3"
     texts = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="none", lm=lm, quality_gate=False,
                                  chunk_bytes=24)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-step", action="store_true")
     ap.add_argument("--configs", action="store_true", help="time every ns_lm_gemm_config tile configuration")
+    ap.add_argument("--kv", default="fp16", choices=["fp16", "fp8"], help="KV cache element type")
+    ap.add_argument("--attn-only", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -48,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         return s.elapsed_time(e) / reps
 
-    lm = BatchedGPT2(random_gpt2(args.model), device=dev, logits_dtype=torch.float16)
+    lm = BatchedGPT2(random_gpt2(args.model), device=dev, logits_dtype=torch.float16, kv_dtype=args.kv)
     s = lm.shape
     C = s.n_embd
     lw = lm.layers[0]
@@ -56,7 +58,7 @@ def main():
     shapes = [("c_attn", lw["qkv_wt"], lw["qkv_b"], lw["qkv_w"], C, 0), ("attn_proj", lw["o_wt"], lw["o_b"], lw["o_w"], C, 2),
               ("c_fc", lw["fc_wt"], lw["fc_b"], lw["fc_w"], C, 1), ("mlp_proj", lw["pr_wt"], lw["pr_b"], lw["pr_w"], 4 * C, 2),
               ("lm_head", lm.head_t, None, lm.head, C, 0)]
-    for name, wt, bias, w, K, epi in shapes:
+    for name, wt, bias, w, K, epi in ([] if args.attn_only else shapes):
         N = wt.shape[0]
         xa = x[:, :K].contiguous()
         y = torch.empty((B, N), device=dev).half()
@@ -105,21 +107,28 @@ def main():
     H, D = s.n_head, C // s.n_head
     lens = [int(v) for v in args.lens.split(",")]
     lm.allocate(B, max(lens) + 2)
-    lm.k_cache[0].normal_()
-    lm.v_cache[0].normal_()
+    if args.kv == "fp8":
+        lm.k_cache[0].random_(0, 120)  # finite e4m3fn bytes (NaN is 0x7f / 0xff)
+        lm.v_cache[0].random_(0, 120)
+    else:
+        lm.k_cache[0].normal_()
+        lm.v_cache[0].normal_()
     qkv = torch.randn((B, 3 * C), device=dev).half()
     o = torch.empty((B, C), device=dev).half()
     for Lc in lens:
         kc, vc = lm.k_cache[0], lm.v_cache[0]
 
+        fn = L.ns_decode_attention_fp8 if args.kv == "fp8" else L.ns_decode_attention_prefix
+
+        sb, sh, sz = lm._cache_strides(0)  # the chunk-plane layout the decode step uses
+
         def attn():
-            rc = L.ns_decode_attention(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
-                                       kc.stride(1), B, H, D, Lc, o.data_ptr(), o.stride(0), D ** -0.5,
-                                       _stream_handle())
+            rc = fn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz, None, None,
+                    0, 0, B, H, D, Lc, None, Lc + 2, o.data_ptr(), o.stride(0), D ** -0.5, _stream_handle())
             assert rc == 0
 
         ms = timed(attn)
-        kv = B * H * (Lc + 1) * D * 2 * 2
+        kv = B * H * (Lc + 1) * D * 2 * (1 if args.kv == "fp8" else 2)
         rec = {"attention_L": Lc, "B": B, "ms": ms, "GBs": kv / ms / 1e6}
         if not args.no_step:
             tok = torch.randint(0, s.vocab, (B,), device=dev)
