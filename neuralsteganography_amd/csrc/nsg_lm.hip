@@ -196,7 +196,13 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
     const int tiles_m = (M + BM - 1) / BM;
     const int tiles_n = (N + BN - 1) / BN;
     const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-    const int tn = t / tiles_m, tm = t - tn * tiles_m;  // m fastest: neighbouring tiles share a weight panel
+    // grouped order: GN weight panels x every activation panel, m fastest inside a group -- the tiles an XCD
+    // runs at once share a few panels of BOTH operands, so both stay in its 4 MiB L2 (m-fastest over all of M
+    // would cycle the whole activation matrix through L2 once per weight panel)
+    constexpr int GN = 1024 / BN;
+    const int grp = t / (GN * tiles_m), within = t - grp * (GN * tiles_m);
+    const int gn = min(GN, tiles_n - grp * GN);
+    const int tm = within / gn, tn = grp * GN + (within - tm * gn);
     const int n0 = tn * BN, m0 = tm * BM;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wn = wave / WM, wm = wave - wn * WM;
@@ -240,22 +246,36 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
         if (s0 < KT) stage(s0, s0);
     int buf = 0;
     for (int kt = 0; kt < KT; ++kt) {
-        // NST - 1 stages ahead: issue tile kt + NST - 1, then wait until tile kt's copies (this thread's) landed
         const int ahead = KT - 1 - kt;  // tiles after kt
-        if (ahead >= NST - 1) {
-            int nb = buf + NST - 1;
-            nb -= nb >= NST ? NST : 0;
-            stage(kt + NST - 1, nb);
-            wait_vm<GL * (NST - 1)>();
-        } else if (NST >= 4 && ahead == 2) {
-            wait_vm<GL * 2>();
-        } else if (NST >= 3 && ahead == 1) {
-            wait_vm<GL>();
+        if constexpr (NST >= 3) {
+            // one barrier per K-tile: wait for this thread's copies of tile kt (the NST-2 younger tiles may stay in
+            // flight), then the barrier both publishes tile kt and certifies that every wave has finished reading
+            // the buffer of tile kt-1, which is the one tile kt+NST-1 is copied into right after it
+            if (ahead >= NST - 2) {
+                wait_vm<GL * (NST - 2)>();
+            } else if (NST >= 4 && ahead == 1) {
+                wait_vm<GL>();
+            } else {
+                wait_vm<0>();
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (ahead >= NST - 1) {
+                int nb = buf + NST - 1;
+                nb -= nb >= NST ? NST : 0;
+                stage(kt + NST - 1, nb);
+            }
         } else {
-            wait_vm<0>();
+            // two buffers: issue tile kt+1, then wait until tile kt's copies (this thread's) landed
+            if (ahead >= 1) {
+                stage(kt + 1, buf ^ 1);
+                wait_vm<GL>();
+            } else {
+                wait_vm<0>();
+            }
+            __builtin_amdgcn_s_barrier();  // ... and every other wave's
+            asm volatile("" ::: "memory");
         }
-        __builtin_amdgcn_s_barrier();  // ... and every other wave's
-        asm volatile("" ::: "memory");
         if constexpr (SPLIT) {
             if (kt > 0 && kt % TPC == 0) {  // a chain ends: fold it into the running total, start the next at 0
 #pragma unroll
@@ -268,26 +288,28 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
             }
         }
         const char* base = smem + buf * ROWS * 128;
+        f16x8 a[2][FN], b[2][FM];  // both 32-wide k-steps of the tile: every LDS read in flight at once
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = kk * 4 + fc;
-            f16x8 a[FN], b[FM];
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
                 const int row = wn * FN * 16 + i * 16 + fr;
-                a[i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+                a[kk][i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
             }
 #pragma unroll
             for (int j = 0; j < FM; ++j) {
                 const int row = BN + wm * FM * 16 + j * 16 + fr;
-                b[j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+                b[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
             }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
-                for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-        }
-        lds_fence_barrier();  // every wave is done reading this buffer before a later tile is copied into it
+                for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[kk][i], b[kk][j], acc[i][j]);
+        if constexpr (NST == 2) lds_fence_barrier();  // every wave is done reading this buffer before it is refilled
         buf = buf + 1 == NST ? 0 : buf + 1;
     }
     if constexpr (SPLIT) {
@@ -423,6 +445,8 @@ enum GemmCfg {
     CFG_T128_2, CFG_T128_3, CFG_T128_4,               // 128 x 128, 4 waves (64 x 64 each)
     CFG_T256x128_2, CFG_T256x128_3,                   // 256 weight rows x 128 activation rows, 8 waves
     CFG_T128x256_2,                                   // 128 x 256, 8 waves
+    CFG_T64_4,                                        // 64 x 64, 4 stages
+    CFG_T128x64_3,                                    // 128 weight rows x 64 activation rows, 4 waves, 3 stages
     CFG_COUNT
 };
 
@@ -471,6 +495,8 @@ static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_
         case CFG_T256x128_2: NSG_TILED(256, 128, 4, 2, 2); break;
         case CFG_T256x128_3: NSG_TILED(256, 128, 4, 2, 3); break;
         case CFG_T128x256_2: NSG_TILED(128, 256, 2, 4, 2); break;
+        case CFG_T64_4: NSG_TILED(64, 64, 2, 2, 4); break;
+        case CFG_T128x64_3: NSG_TILED(128, 64, 2, 2, 3); break;
 #undef NSG_DIRECT
 #undef NSG_TILED
         default: break;
