@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
     ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
     ap.add_argument("--fp8kv", action="store_true", help="add the fp8-KV-cache end-to-end side line (opt-in mode)")
+    ap.add_argument("--optin-window", type=int, default=256,
+                    help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-logits (PCIe-inclusive) side figure")
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
@@ -148,7 +150,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
-def end_to_end(args, rank, world, dev, kv_dtype="fp16"):
+def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0):
     """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
     compute, HIP decode attention) + HIP coder step per token, every stream encoding its full payload from
     the shared 32-token context until the last stream is done (lockstep, like the reference's per-message
@@ -165,7 +167,7 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16"):
     if args.blas:
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
-                         max_batch=B, kv_dtype=kv_dtype)
+                         max_batch=B, kv_dtype=kv_dtype, attention_window=window)
     lm.lm.position_cap = args.e2e_kv_cap
     lm.lm.chunked_cache = args.e2e_kv_layout == "chunked"
     quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
@@ -198,11 +200,11 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16"):
            "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max,
            "lockstep_steps": steps, "ms_per_step": 1e3 * el_max / steps, "bits_per_token": bits_all / tok_all,
            "kv_positions": lm.lm.max_len,
-           "kv_dtype": kv_dtype,
+           "kv_dtype": kv_dtype, "attention_window": window or None,
            "workload": f"{args.e2e_model} (random-init weights, fp16 compute, {args.e2e_logits} logits, {kv_dtype} KV "
                        f"cache, batch-invariant native decode step) + ns_encode_step, {B} streams/GPU x "
                        f"{args.e2e_payload_bytes}-byte payloads encoded to completion from a 32-token context, "
-                       f"unbounded KV cache"}
+                       + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")}
     del lm
     torch.cuda.empty_cache()
     return out
@@ -372,6 +374,8 @@ def main():
         out["end_to_end"] = end_to_end(args, rank, world, dev)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             out["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
+        if args.optin_window:  # opt-in: fp8 KV + sliding attention window (bounded per-step KV traffic)
+            out["end_to_end_optin"] = end_to_end(args, rank, world, dev, kv_dtype="fp8", window=args.optin_window)
     if want_cpu:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_baseline_seconds)
     if rank == 0:

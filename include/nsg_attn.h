@@ -50,12 +50,14 @@ int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
  * the cache's capacity (fewer pages touched).  `cap` = total positions (prefix + the stream cache's rows); the
  * new token is written at stream index L0 - T0.  L0 comes from *d_L0 when d_L0 is not NULL (graph replays),
  * else from the argument.  T0 = 0 is ns_decode_attention(_dev).  The output bits do not depend on where a
- * row is stored (same values, same order). */
+ * row is stored (same values, same order).  window > 0 (opt-in; 0 = the reference's unbounded attention) attends
+ * to the last `window` positions only, [max(0, L0 + 1 - window), L0]: a sliding-window approximation that bounds
+ * the per-step KV traffic (NOT the reference's max_context, which re-runs a trimmed context). */
 int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                                int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                                const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B,
-                               int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out, int64_t out_stride,
-                               float scale, void* hip_stream);
+                               int H, int D, int L0, const int32_t* d_L0, int cap, int window, void* d_out,
+                               int64_t out_stride, float scale, void* hip_stream);
 
 /* ns_decode_attention_prefix over an fp8 KV cache (OCP e4m3fn bytes, element layout as above with 1-byte
  * elements): half the HBM bytes of the fp16 cache.  The new token's k/v are quantised (saturated to +-448,
@@ -65,8 +67,8 @@ int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_
 int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                             int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                             const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B,
-                            int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out, int64_t out_stride,
-                            float scale, void* hip_stream);
+                            int H, int D, int L0, const int32_t* d_L0, int cap, int window, void* d_out,
+                            int64_t out_stride, float scale, void* hip_stream);
 
 /* fp16 [n] -> fp8 e4m3fn [n] with the attention's conversion (n % 4 == 0, 8-byte aligned). */
 int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream);

@@ -128,8 +128,8 @@ def lib() -> ctypes.CDLL:
     for name in ("ns_decode_attention_prefix", "ns_decode_attention_fp8"):
         f = getattr(L, name)
         f.restype = ci
-        f.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, vp, i64, ctypes.c_float,
-                      vp]
+        f.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, vp, i64,
+                      ctypes.c_float, vp]
     L.ns_quantize_fp8.restype = ci
     L.ns_quantize_fp8.argtypes = [vp, vp, i64, vp]
     L.ns_lm_gemm.restype = ci

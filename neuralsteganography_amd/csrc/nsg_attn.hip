@@ -154,8 +154,8 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                                                           int64_t ch, int64_t cz, const typename F::Elem* __restrict__ kp,
                                                           const typename F::Elem* __restrict__ vp, int64_t ph, int T0,
                                                           int B, int H, int L0, const int32_t* __restrict__ L0p,
-                                                          int cap, _Float16* __restrict__ out, int64_t out_stride,
-                                                          float scale_log2) {
+                                                          int cap, int window, _Float16* __restrict__ out,
+                                                          int64_t out_stride, float scale_log2) {
     typedef typename F::Elem E;
     typedef typename F::Raw Raw;
     constexpr int DPL = F::DPL, LPR = F::LPR, RPI = F::RPI, NI = F::NI;
@@ -164,7 +164,9 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     __shared__ float s_m[8], s_l[8];
     __shared__ float s_acc[8][ATT_D];
     const int Lk = L0 + 1;
-    const int S = att_split(Lk);
+    // attention window (opt-in, 0 = the reference's unbounded cache): keys [s0, L0], s0 = max(0, L0 + 1 - window)
+    const int s0 = window > 0 ? max(0, Lk - window) : 0;
+    const int S = att_split(Lk - s0);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int grp = wave / S, wv = wave - grp * S, ngrp = 8 / S;
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                 }
                 m = mx;
             };
-            for (int j0 = wv * RPI * NI; j0 < Lk; j0 += S * RPI * NI) {
+            for (int j0 = s0 + wv * RPI * NI; j0 < Lk; j0 += S * RPI * NI) {
                 if (j0 >= T0 && j0 + RPI * NI <= L0)  // wave-uniform
                     chunk(j0, std::false_type{});
                 else
@@ -335,9 +337,10 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
                             int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                             const void* d_k_prefix,
                             const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
-                            const int32_t* d_L0, int cap, void* d_out, int64_t out_stride, float scale,
+                            const int32_t* d_L0, int cap, int window, void* d_out, int64_t out_stride, float scale,
                             void* hip_stream) {
     typedef typename F::Elem E;
+    if (window < 0) return NS_ERR_CONFIG;
     if (!d_qkv || !d_k_cache || !d_v_cache || !d_out || B <= 0 || H <= 0 || L0 < 0 || T0 < 0) return NS_ERR_CONFIG;
     if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
     constexpr int ALIGN_E = 16 / (int)sizeof(E);  // elements per 16-byte unit of the cache
@@ -378,11 +381,11 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     if (pairs <= NSG_ATT_SMALL_PAIRS)
         hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 1>), dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
                            cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B, H,
-                           L0, d_L0, cap, o, out_stride, scale_log2);
+                           L0, d_L0, cap, window, o, out_stride, scale_log2);
     else
         hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 8>), dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k,
                            v, cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B,
-                           H, L0, d_L0, cap, o, out_stride, scale_log2);
+                           H, L0, d_L0, cap, window, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
@@ -390,7 +393,7 @@ extern "C" int ns_decode_attention(const void* d_qkv, int64_t qkv_stride, void* 
                                    int64_t cache_b_stride, int64_t cache_h_stride, int B, int H, int D, int L0,
                                    void* d_out, int64_t out_stride, float scale, void* hip_stream) {
     return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, 0,
-                                         nullptr, nullptr, 0, 0, B, H, D, L0, nullptr, L0 + 1, d_out, out_stride,
+                                         nullptr, nullptr, 0, 0, B, H, D, L0, nullptr, L0 + 1, 0, d_out, out_stride,
                                          scale, hip_stream);
 }
 
@@ -400,28 +403,28 @@ extern "C" int ns_decode_attention_dev(const void* d_qkv, int64_t qkv_stride, vo
                                        void* hip_stream) {
     if (!d_L0 || cap < 1) return NS_ERR_CONFIG;
     return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride, 0,
-                                         nullptr, nullptr, 0, 0, B, H, D, 0, d_L0, cap, d_out, out_stride, scale,
+                                         nullptr, nullptr, 0, 0, B, H, D, 0, d_L0, cap, 0, d_out, out_stride, scale,
                                          hip_stream);
 }
 
 extern "C" int ns_decode_attention_prefix(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                                           int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                                           const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride,
-                                          int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap,
+                                          int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap, int window,
                                           void* d_out, int64_t out_stride, float scale, void* hip_stream) {
     return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
                                          cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
-                                         d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+                                         d_L0 ? 0 : L0, d_L0, cap, window, d_out, out_stride, scale, hip_stream);
 }
 
 extern "C" int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                                        int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                                        const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride,
-                                       int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap, void* d_out,
-                                       int64_t out_stride, float scale, void* hip_stream) {
+                                       int T0, int B, int H, int D, int L0, const int32_t* d_L0, int cap, int window,
+                                       void* d_out, int64_t out_stride, float scale, void* hip_stream) {
     return decode_attention<nsg::FmtF8>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
                                         cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
-                                        d_L0 ? 0 : L0, d_L0, cap, d_out, out_stride, scale, hip_stream);
+                                        d_L0 ? 0 : L0, d_L0, cap, window, d_out, out_stride, scale, hip_stream);
 }
 
 extern "C" int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream) {

@@ -91,6 +91,9 @@ class BatchedGPT2:
         self.T0 = 0  # positions held once in the shared prefix cache (kp, vp) instead of per stream
         self.position_cap = None  # optional cap on the initial per-stream cache length (the cache still grows)
         self.chunked_cache = True  # native decode: chunk-plane KV layout (False: plain per-pair rows; A/B only)
+        # attention window (opt-in, 0 = the reference's unbounded cache): decode steps attend to the last `window`
+        # positions only -- a sliding-window approximation bounding the per-step KV traffic (native path only)
+        self.window = 0
         self.kp = self.vp = None
         self.k_cache = self.v_cache = None
         # Decode steps in fp16 on the GPU run entirely on the batch-invariant HIP kernels (include/nsg_lm.h and
@@ -374,7 +377,7 @@ class BatchedGPT2:
             vp = self.vp[i, 0] if T0 else None
             rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz,
                             kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
-                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, o.data_ptr(),
+                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, self.window, o.data_ptr(),
                             o.stride(0), 1.0 / math.sqrt(D), st)
             ok(rc, "ns_decode_attention_prefix")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)

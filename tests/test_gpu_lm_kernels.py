@@ -227,7 +227,7 @@ def test_prefix_attention_equals_full_cache(T0, L0, dev):
     dL = torch.tensor([L0], dtype=torch.int32, device="cuda")
     assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
                                           ks.stride(1), 0, kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
-                                          -1 if dev else L0, dL.data_ptr() if dev else None, cap, got.data_ptr(),
+                                          -1 if dev else L0, dL.data_ptr() if dev else None, cap, 0, got.data_ptr(),
                                           got.stride(0), D ** -0.5, _stream_handle()) == 0
     torch.cuda.synchronize()
     assert torch.equal(got, want)
@@ -235,7 +235,7 @@ def test_prefix_attention_equals_full_cache(T0, L0, dev):
     # a position inside the prefix cannot be appended
     assert lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
                                           ks.stride(1), 0, kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D,
-                                          T0 - 1, None, cap, got.data_ptr(), got.stride(0), D ** -0.5,
+                                          T0 - 1, None, cap, 0, got.data_ptr(), got.stride(0), D ** -0.5,
                                           None) == _lib.NS_ERR_CONFIG
 
 
@@ -267,7 +267,7 @@ def test_chunk_plane_layout_equals_plain(kv, T0, L0):
                           (chunk_k, chunk_v, (chunk_k.stride(1), chunk_k.stride(2), chunk_k.stride(0)))):
         o = torch.empty((B, H * D), device="cuda").half()
         assert f(qkv.data_ptr(), qkv.stride(0), k.data_ptr(), v.data_ptr(), *strides, kp.data_ptr() if T0 else None,
-                 vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D, L0, None, cap, o.data_ptr(),
+                 vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D, L0, None, cap, 0, o.data_ptr(),
                  o.stride(0), D ** -0.5, _stream_handle()) == 0
         outs.append(o)
     torch.cuda.synchronize()
@@ -361,7 +361,7 @@ def test_fp8_attention_matches_fp32_reference(B, L0, T0):
     rc = _lib.lib().ns_decode_attention_fp8(qkv.data_ptr(), qkv.stride(0), ks.data_ptr(), vs.data_ptr(), ks.stride(0),
                                             ks.stride(1), 0, kp.data_ptr() if T0 else None,
                                             vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D, L0,
-                                            None, cap, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle())
+                                            None, cap, 0, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle())
     assert rc == 0
     torch.cuda.synchronize()
     q, k, v = qkv.view(B, 3, H, D).unbind(1)
@@ -385,11 +385,11 @@ def test_fp8_attention_is_batch_invariant():
     f = _lib.lib().ns_decode_attention_fp8
     out = torch.empty((B, H * D), device="cuda").half()
     assert f(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), 0, None, None,
-             0, 0, B, H, D, L0, None, L0 + 2, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle()) == 0
+             0, 0, B, H, D, L0, None, L0 + 2, 0, out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle()) == 0
     for b in (0, 150, 299):
         o1 = torch.empty((1, H * D), device="cuda").half()
         assert f(qkv[b:].data_ptr(), qkv.stride(0), kc[b:].data_ptr(), vc[b:].data_ptr(), kc.stride(0), kc.stride(1),
-                 0, None, None, 0, 0, 1, H, D, L0, None, L0 + 2, o1.data_ptr(), o1.stride(0), D ** -0.5,
+                 0, None, None, 0, 0, 1, H, D, L0, None, L0 + 2, 0, o1.data_ptr(), o1.stride(0), D ** -0.5,
                  _stream_handle()) == 0
         torch.cuda.synchronize()
         assert torch.equal(o1[0], out[b]), b
@@ -425,6 +425,74 @@ def test_fp8_kv_cover_batch_reveals_alone():
     lm = HipArithmeticLM(m, IdTokenizer(2000), compute_dtype=torch.float16, logits_dtype="f16", kv_dtype="fp8")
     q = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": False}
     secrets = [b"fp8 cache", bytes(range(40)), b"x"]
+    seed = "w5. w6. w3"
+    texts = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="none", lm=lm, quality_gate=False,
+                                 chunk_bytes=24)
+    for text, secret in zip(texts, secrets):
+        assert cover_reveal(text, seed_text=seed, quality=q, ecc="none", lm=lm) == secret
+
+
+# --------------------------------------------------------------------------------- attention window (opt-in)
+@pytest.mark.parametrize("kv", ["fp16", "fp8"])
+@pytest.mark.parametrize("T0,L0,W", [(32, 40, 16), (32, 300, 64), (32, 300, 290), (5, 1000, 200), (0, 77, 1),
+                                     (32, 31 + 5, 100)])
+def test_window_attention_matches_reference(kv, T0, L0, W):
+    """window > 0: softmax over the last W positions [max(0, L0 + 1 - W), L0] only (prefix rows included while
+    inside the window), vs fp32 torch; the output is batch-invariant (B = 1 vs B = 30)."""
+    B, H, D = 30, 12, 64
+    cap = L0 + 3
+    g = torch.Generator(device="cuda").manual_seed(T0 + L0 + W)
+    qkv = torch.randn((B, 3 * H * D), generator=g, device="cuda").half()
+    kf = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    vf = torch.randn((B, H, cap, D), generator=g, device="cuda").half()
+    if kv == "fp8":
+        kq, vq = _q8(kf), _q8(vf)
+        deq = _dq8
+        f = _lib.lib().ns_decode_attention_fp8
+        knew, vnew = _dq8(_q8(qkv.view(B, 3, H, D)[:, 1])), _dq8(_q8(qkv.view(B, 3, H, D)[:, 2]))
+    else:
+        kq, vq = kf, vf
+        deq = lambda t: t.float()  # noqa: E731
+        f = _lib.lib().ns_decode_attention_prefix
+        knew, vnew = qkv.view(B, 3, H, D)[:, 1].float(), qkv.view(B, 3, H, D)[:, 2].float()
+    kp, vp = kq[0, :, :T0].contiguous(), vq[0, :, :T0].contiguous()
+    ks, vs = kq[:, :, T0:].contiguous(), vq[:, :, T0:].contiguous()
+
+    def run(b0, nb):
+        o = torch.empty((nb, H * D), device="cuda").half()
+        assert f(qkv[b0:].data_ptr(), qkv.stride(0), ks[b0:].data_ptr(), vs[b0:].data_ptr(), ks.stride(0), ks.stride(1),
+                 0, kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, nb, H,
+                 D, L0, None, cap, W, o.data_ptr(), o.stride(0), D ** -0.5, _stream_handle()) == 0
+        return o
+
+    out = run(0, B)
+    one = run(7, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(one[0], out[7])
+    kk = torch.cat([kp[None].expand(B, -1, -1, -1), ks], dim=2) if T0 else ks
+    vv = torch.cat([vp[None].expand(B, -1, -1, -1), vs], dim=2) if T0 else vs
+    kk, vv = deq(kk.contiguous()).clone(), deq(vv.contiguous()).clone()
+    kk[:, :, L0], vv[:, :, L0] = knew, vnew
+    s0 = max(0, L0 + 1 - W)
+    q = qkv.view(B, 3, H, D)[:, 0].float()
+    sc = torch.einsum("bhd,bhjd->bhj", q, kk[:, :, s0: L0 + 1]) * D ** -0.5
+    want = torch.einsum("bhj,bhjd->bhd", torch.softmax(sc, -1), vv[:, :, s0: L0 + 1]).reshape(B, H * D)
+    assert (out.float() - want).abs().max().item() < 2e-3
+
+
+def test_window_cover_batch_reveals_alone():
+    """The opt-in modes together (fp8 KV cache + a 24-position attention window, shorter than the covers): covers
+    from cover_generate_batch reveal one by one."""
+    from neuralsteganography_amd.cover import cover_generate_batch, cover_reveal
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from test_gpu_guard import IdTokenizer
+
+    m = random_gpt2("tiny", vocab_size=2000, n_positions=1024, n_embd=128, n_head=2, seed=31)
+    lm = HipArithmeticLM(m, IdTokenizer(2000), compute_dtype=torch.float16, logits_dtype="f16", kv_dtype="fp8",
+                         attention_window=24)
+    q = {"temp": 0.9, "precision": 26, "topk": 300, "finish_sent": False}
+    secrets = [b"windowed attention", bytes(range(50)), b"w"]
     seed = "w5. w6. w3"
     texts = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="none", lm=lm, quality_gate=False,
                                  chunk_bytes=24)

@@ -124,7 +124,7 @@ def main():
 
         def attn():
             rc = fn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz, None, None,
-                    0, 0, B, H, D, Lc, None, Lc + 2, o.data_ptr(), o.stride(0), D ** -0.5, _stream_handle())
+                    0, 0, B, H, D, Lc, None, Lc + 2, 0, o.data_ptr(), o.stride(0), D ** -0.5, _stream_handle())
             assert rc == 0
 
         ms = timed(attn)
