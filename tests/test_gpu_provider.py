@@ -280,3 +280,51 @@ def test_graph_captured_encode_matches_eager(cap_extra, topk, n):
         assert all(d[: len(b)] == b for d, b in zip(dec, bits))
         out[("dec", graphs)] = dec
     assert out[True] == out[False] and out[("dec", True)] == out[("dec", False)]
+
+
+def test_coder_context_cache_reuses_and_bounds():
+    """coder contexts are keyed on the parameters only -- a context built for a larger batch
+    serves smaller ones, a larger batch replaces it, and at most CTX_CACHE_SIZE parameter sets stay alive."""
+    from neuralsteganography_amd.coder import CoderParams
+    from neuralsteganography_amd.lm import arithmetic as arith
+
+    _, lm = _tiny_provider()
+    p = CoderParams(vocab=lm.vocab, precision=26, temp=0.9, topk=300, dtype="f32")
+    c8 = lm._coder(p, 8)
+    assert lm._coder(p, 3) is c8 and c8.max_batch == 8  # smaller batch: same context
+    c16 = lm._coder(p, 16)
+    assert c16 is not c8 and c16.max_batch == 16 and c8._h is None  # replaced and closed
+    for t in range(arith.CTX_CACHE_SIZE + 2):  # distinct parameter sets: LRU-bounded
+        lm._coder(CoderParams(vocab=lm.vocab, precision=26, temp=0.5 + 0.1 * t, topk=300, dtype="f32"), 4)
+    assert len(lm._ctx_cache) == arith.CTX_CACHE_SIZE
+    assert c16._h is None  # the oldest one was evicted and closed
+
+
+def test_stop_text_stops_inside_graph_replay():
+    """the '<eos>' stop of the code_base entry points runs with the hipGraph-captured step (a
+    device table of ids that can complete the stop text + one flag per token); the stopped stream's tokens end
+    with the stop text, as the reference's decoded-text check stops (code_base/arithmetic.py:207-210)."""
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    class TwoCharTok:
+        """ids < 256: a byte; id 300: '<eos>' as one token (so the stop fires exactly when it is emitted)."""
+
+        def decode(self, ids):
+            return "".join("<eos>" if int(i) == 300 else chr(int(i) % 256) for i in ids)
+
+        def encode(self, text, add_special_tokens=False):
+            return [ord(ch) for ch in text]
+
+    m = random_gpt2("tiny", vocab_size=512, n_positions=512, n_embd=128, n_head=2, seed=3)
+    lm = HipArithmeticLM(m, TwoCharTok(), compute_dtype=torch.float16, logits_dtype="f32")
+    # a wide temperature flattens the random LM so id 300 shows up within a few hundred tokens for some streams
+    q = {"temp": 3.0, "precision": 26, "topk": 500}
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 384)) for s in range(8)]
+    toks_g = lm.encode_batch(bits, [1, 2, 3], quality=q, stop_text="<eos>", graphs=True)
+    toks_e = lm.encode_batch(bits, [1, 2, 3], quality=q, stop_text="<eos>", graphs=False)
+    assert toks_g == toks_e
+    stopped = [t for t in toks_g if 300 in t]
+    assert stopped, "no stream emitted the stop token: pick another seed"
+    for t in stopped:
+        assert t[-1] == 300 and t.count(300) == 1  # stops right after the first '<eos>'
