@@ -12,10 +12,11 @@
  * tile shape chosen for M:
  *
  *   ns_lm_gemm       Y = epilogue(X . Wt^T + bias): one MFMA instruction (v_mfma_f32_16x16x32_f16) for every
- *                    shape, output element (m, n) at MFMA position (n mod 16, m mod 16), K accumulated in
- *                    ascending 32-wide steps into one fp32 chain, no split-K; the tile (16 x 16..64 direct
- *                    loads for small M, 64x64 / 128x128 LDS tiles for large M) changes only WHICH wave
- *                    computes an element, never how.
+ *                    shape, output element (m, n) at MFMA position (n mod 16, m mod 16); K cut by K ALONE
+ *                    into 1, 2 or 4 consecutive ranges (K <= 1024 / <= 2048 / larger), each accumulated in
+ *                    ascending 32-wide steps into one fp32 chain from zero, the chains added in order; the
+ *                    tile (16 x 16..64 direct loads for small M, 64x64 .. 256x128 LDS tiles for large M)
+ *                    changes only WHICH wave computes an element, never how.
  *   ns_lm_layernorm  one wavefront per row, fixed per-lane order + xor butterfly for mean and variance.
  *   ns_lm_embed_ln   h = wte[token] + wpe[pos] (fp16) and ln_1(h) in one pass (pos = L mod n_positions,
  *                    code_base/arithmetic.py:44-48; L from the host or from device memory for graph replays).

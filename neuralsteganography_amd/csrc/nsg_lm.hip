@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
     f32x4 acc[FM];
 #pragma unroll
     for (int f = 0; f < FM; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    constexpr int U = FM == 1 ? 16 : 8;  // 32-wide k-steps per batch of loads in flight
+    constexpr int U = FM == 1 ? 24 : FM == 2 ? 12 : 8;  // 32-wide k-steps per batch of loads in flight (K = 768: one)
     int k = k_begin;
     if (live) {
         for (; k + 32 * U <= k_end; k += 32 * U) {
@@ -128,6 +128,9 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
 #pragma unroll
                 for (int f = 0; f < FM; ++f) b[u][f] = *(const f16x8*)(xrow[f] + k + 32 * u);
             }
+            // keep every load of the batch ahead of the MFMAs (the scheduler would otherwise interleave them to
+            // save registers, leaving a dozen in flight: at small M each batch costs one memory round trip)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
