@@ -63,6 +63,8 @@ def parse():
                     help="GEMM library for the GPT-2 forward (torch.backends.cuda.preferred_blas_library)")
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
                     help="logits handed to the coder; the fp16 head GEMM's output either way (f32 = upcast copy)")
+    ap.add_argument("--eager", action="store_true",
+                    help="time eager launches (one event pair each) instead of the replayed hipGraph of the K steps")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch measured by a rocprofv3 --pmc pass (corrected), if known")
     return ap.parse_args()
@@ -291,18 +293,47 @@ def main():
     for t in range(args.warmup):
         sess.step(pool[t % args.pool])
     torch.cuda.synchronize()
+    # side figure: eager launches with one HIP event pair per launch (the per-launch kernel time rocprofv3 sees)
+    n_eager = 0 if args.eager else min(args.steps, 50)
+    eager = None
+    if n_eager:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_eager)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(n_eager):
+            ev[t][0].record(stream)
+            sess.step(pool[(args.warmup + t) % args.pool])
+            ev[t][1].record(stream)
+        torch.cuda.synchronize()
+        eager = {"ms_per_step": 1e3 * (time.perf_counter() - t0) / n_eager,
+                 "kernel_ms_avg": float(np.mean([a.elapsed_time(b) for a, b in ev])), "steps": n_eager}
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph = None
+    if not args.eager:
+        # headline: the K timed steps captured once as a hipGraph and replayed (as the product's token loop
+        # replays its captured step), so the step time is the launches' own, without host launch gaps
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for t in range(args.steps):
+                sess.step(pool[(args.warmup + n_eager + t) % args.pool])
+    torch.cuda.synchronize()
     f0 = sess.fields()
     c0 = ctx.counters()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(args.steps):
-        ev[t][0].record(stream)
-        sess.step(pool[(args.warmup + t) % args.pool])
-        ev[t][1].record(stream)
+    if graph is not None:
+        g0.record(stream)
+        graph.replay()
+        g1.record(stream)
+    else:
+        for t in range(args.steps):
+            ev[t][0].record(stream)
+            sess.step(pool[(args.warmup + t) % args.pool])
+            ev[t][1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -310,7 +341,11 @@ def main():
 
     f1 = sess.fields()
     c1 = ctx.counters()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if graph is not None:  # per-launch average over the replay (launch gaps of a graph included)
+        kern_ms = g0.elapsed_time(g1) / args.steps
+        del graph
+    else:
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     stream_steps = int(f1["ntokens"].sum() - f0["ntokens"].sum())
     exact_steps = c1[0] - c0[0]
     overflow_compactions = c1[1] - c0[1]
@@ -355,6 +390,9 @@ def main():
         "cover_tokens_per_s": ss_all / elapsed_max,
         "bits_per_token": bits_all / max(ss_all, 1.0),
         "kernel_ms_avg": kern_ms,
+        "timing": ("K launches captured in one hipGraph, replayed once; kernel_ms_avg = replay time / K (HIP "
+                   "events on the launch stream)") if not args.eager else "eager launches, one event pair each",
+        "eager_launches": eager,  # the first min(K, 50) steps after the warm-up, launched one by one
         "exact_sum_fraction": exact_steps / max(stream_steps, 1),
         "overflow_compactions_per_stream_step": overflow_compactions / max(stream_steps, 1),
         "speculation_miss_fraction": spec_misses / max(stream_steps, 1),

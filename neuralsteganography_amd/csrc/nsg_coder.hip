@@ -39,11 +39,16 @@
 #ifndef NSG_SAMPLE
 #define NSG_SAMPLE 16  // stratified sample: this many 64-id blocks (values per lane) for the speculative threshold
 #endif
+#ifndef NSG_FMA_ARG
+#define NSG_FMA_ARG 1  // fast-sum exponent as one fma (x*c - r*c) with packed / two-chain fp32 sums
+#endif
 #ifndef NSG_BUCKET_CAP
 #define NSG_BUCKET_CAP 48  // largest bucket the bucket rank accepts (its fix-up loop runs that often)
 #endif
 
 namespace nsg {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Per-wave LDS scratch: 256+4 bucket counters/bases (u32), 64 gathered keys (u64), and a slow-path counter.
 constexpr int SCR_U32 = 392;
@@ -618,19 +623,42 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     }
     // fp32 partial sums of one group, flushed into float64 (STATS adds sum e*(x-r) and the untempered sum;
     // masked ids are -inf: dx is clamped so e*dx is 0, not NaN)
+    // Plain builds take the exponent as ONE fma, x*c32 - fl(r*c32) (fp16 rows: v_fma_mix, the conversion
+    // included; fp32 rows: packed pairs), and sum in two fp32 chains; the bound below adds u*|r*c32|.
+    const float nrc = -(r * c32);
     auto accumulate = [&](const float* xs, int n) {
         float a = 0.0f, bb = 0.0f, uu = 0.0f;
+        if (STATS) {
 #pragma unroll
-        for (int i = 0; i < n; ++i) {
-            if (STATS) {
+            for (int i = 0; i < n; ++i) {
                 const float dx = fmaxf(xs[i] - r, -3.0e38f);
                 const float e = __builtin_amdgcn_exp2f(dx * c32);
                 a += e;
                 bb += e * dx;
                 uu += __builtin_amdgcn_exp2f(dx * L2E_F);
-            } else {
-                a += __builtin_amdgcn_exp2f((xs[i] - r) * c32);
             }
+        } else if (NSG_FMA_ARG && W == 4) {
+            f32x2 a2 = {0.0f, 0.0f};
+            const f32x2 c2 = {c32, c32}, n2 = {nrc, nrc};
+#pragma unroll
+            for (int i = 0; i < n; i += 2) {
+                const f32x2 x2 = {xs[i], xs[i + 1]};
+                const f32x2 t = __builtin_elementwise_fma(x2, c2, n2);
+                const f32x2 e2 = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+                a2 += e2;
+            }
+            a = a2.x + a2.y;
+        } else if (NSG_FMA_ARG) {
+            float a1 = 0.0f;
+#pragma unroll
+            for (int i = 0; i < n; i += 2) {
+                a += __builtin_amdgcn_exp2f(__builtin_fmaf(xs[i], c32, nrc));
+                a1 += __builtin_amdgcn_exp2f(__builtin_fmaf(xs[i + 1], c32, nrc));
+            }
+            a += a1;
+        } else {
+#pragma unroll
+            for (int i = 0; i < n; ++i) a += __builtin_amdgcn_exp2f((xs[i] - r) * c32);
         }
         acc64 += (double)a;
         if (STATS) {
@@ -780,7 +808,8 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         const double Sf = S_r * f;
         const double u24 = 5.9604644775390625e-08;  // 2^-24
         const double eb = 9.5367431640625e-07         // v_exp_f32 error (2^-20, generous)
-                          + 3.0 * u24 * 0.6931471805599453 * (60.0 + fabs(t_m))  // argument rounding
+                          + 3.0 * u24 * 0.6931471805599453 *                     // argument rounding
+                                (60.0 + fabs(t_m) + (STATS || !NSG_FMA_ARG ? 0.0 : fabs((double)nrc)))
                           + (double)(PREFETCH * W + 1) * u24                        // fp32 partials
                           + 1.0e-13;
         const double B2 = 2.0 * eb + 1.0e-12;
