@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=6, help="distinct logit batches cycled over the steps")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-e2e-seconds", type=float, default=10.0,
+                    help="end-to-end CPU baseline (HF GPT-2 forward + oracle coder per core); 0 = skip")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
     ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
     ap.add_argument("--fp8kv", action="store_true", help="add the fp8-KV-cache end-to-end side line (opt-in mode)")
@@ -70,34 +72,58 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, seconds, streams_per_core=16):
-    """The oracle port timed on the host cores on a bounded sample of the same workload (BASELINE.md: one
-    process per core, the core count from the affinity mask, capped at the box's 16-CPU share).  Each worker is
-    a child process (``python -m oracle.cpu_baseline``) that never touches the GPU and encodes its own streams
-    of 3·N(0,1) fp32 rows for ``seconds``; bits and stream-steps are summed, the time is the slowest worker's."""
+def _cpu_workers(module, argv, seconds):
+    """One child process per host core (the affinity mask, capped at the box's 16-CPU share), each running
+    ``python -m <module> <argv...>`` on one thread; returns (cores, parsed JSON results)."""
     import subprocess
 
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
     env = dict(os.environ, OMP_NUM_THREADS="1")
     procs = []
     for c in range(cores):
-        cmd = [sys.executable, "-m", "oracle.cpu_baseline", str(seconds), str(streams_per_core), str(1000 + c),
-               str(args.vocab), str(args.temp), str(args.precision), str(args.topk), str(args.payload_bytes)]
+        cmd = [sys.executable, "-m", module] + [str(a) for a in argv(c)]
         procs.append(subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=subprocess.PIPE, text=True))
     res = []
     for pr in procs:
-        text, _ = pr.communicate(timeout=seconds * 4 + 120)
+        text, _ = pr.communicate(timeout=seconds * 4 + 180)
         if pr.returncode != 0:
-            raise RuntimeError(f"cpu_baseline worker failed ({pr.returncode})")
+            raise RuntimeError(f"{module} worker failed ({pr.returncode})")
         res.append(json.loads(text.strip().splitlines()[-1]))
+    return cores, res
+
+
+def cpu_baseline(args, seconds, streams_per_core=16):
+    """The oracle port timed on the host cores on a bounded sample of the same workload (BASELINE.md: one
+    process per core, the core count from the affinity mask, capped at the box's 16-CPU share).  Each worker is
+    a child process (``python -m oracle.cpu_baseline``) that never touches the GPU and encodes its own streams
+    of 3·N(0,1) fp32 rows for ``seconds``; bits and stream-steps are summed, the time is the slowest worker's.
+    ``end_to_end`` adds BASELINE.md's second number: the reference's token loop (batch 1, Hugging Face GPT-2-small
+    forward with the KV cache, random-init fp32) + the oracle coder per core (``oracle/cpu_e2e.py``)."""
+    cores, res = _cpu_workers("oracle.cpu_baseline", lambda c: [seconds, streams_per_core, 1000 + c, args.vocab,
+                                                                args.temp, args.precision, args.topk,
+                                                                args.payload_bytes], seconds)
     dt = max(r["seconds"] for r in res)
     bits = sum(r["bits"] for r in res)
     ss = sum(r["stream_steps"] for r in res)
-    return {"value": bits / dt, "unit": "payload bits/s", "cores": cores, "kind": "port",
-            "cover_tokens_per_s": ss / dt, "per_core_bits_per_s": bits / dt / cores,
-            "sample": f"oracle/nsg_oracle.c or_encode_batch: {cores} worker processes (1 core each) x "
-                      f"{streams_per_core} streams of 3N(0,1) fp32 rows, V {args.vocab}, topk {args.topk}, "
-                      f"{args.payload_bytes}-byte payloads, {dt:.1f} s"}
+    out = {"value": bits / dt, "unit": "payload bits/s", "cores": cores, "kind": "port",
+           "cover_tokens_per_s": ss / dt, "per_core_bits_per_s": bits / dt / cores,
+           "sample": f"oracle/nsg_oracle.c or_encode_batch: {cores} worker processes (1 core each) x "
+                     f"{streams_per_core} streams of 3N(0,1) fp32 rows, V {args.vocab}, topk {args.topk}, "
+                     f"{args.payload_bytes}-byte payloads, {dt:.1f} s"}
+    if args.cpu_e2e_seconds > 0:
+        cores, res = _cpu_workers("oracle.cpu_e2e", lambda c: [args.cpu_e2e_seconds, 2000 + c, args.vocab,
+                                                               args.temp, args.precision, args.topk,
+                                                               args.payload_bytes], args.cpu_e2e_seconds)
+        dt = max(r["seconds"] for r in res)
+        bits = sum(r["bits"] for r in res)
+        tok = sum(r["tokens"] for r in res)
+        out["end_to_end"] = {
+            "value": bits / dt, "unit": "payload bits/s", "cores": cores, "cover_tokens_per_s": tok / dt,
+            "cover_tokens_per_s_per_core": tok / dt / cores, "bits_per_token": bits / max(tok, 1),
+            "sample": f"{cores} worker processes (1 thread each), each the reference's batch-1 token loop: HF "
+                      f"GPT2LMHeadModel (random-init GPT-2-small, fp32, KV cache) + oracle or_encode_batch, "
+                      f"{args.payload_bytes}-byte payloads, {dt:.1f} s; model construction excluded"}
+    return out
 
 
 def wide_path(args, rank, world, dev, steps=10, warmup=3):
