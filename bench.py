@@ -187,7 +187,7 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0):
     import torch.distributed as dist
 
     from neuralsteganography_amd import synthetic
-    from neuralsteganography_amd.dist import reduce_job, shard_range
+    from neuralsteganography_amd.dist import per_rank, reduce_job, shard_range
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
@@ -224,8 +224,10 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0):
     ntok = sum(len(t) for t in toks)
     steps = max(len(t) for t in toks)
     bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
+    rank_s, rank_steps = per_rank(elapsed, device=dev), per_rank(steps, device=dev)
     out = {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
            "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max,
+           "per_rank_seconds": rank_s, "per_rank_lockstep_steps": [int(v) for v in rank_steps],
            "lockstep_steps": steps, "ms_per_step": 1e3 * el_max / steps, "bits_per_token": bits_all / tok_all,
            "kv_positions": lm.lm.max_len,
            "kv_dtype": kv_dtype, "attention_window": window or None,
@@ -309,7 +311,7 @@ def main():
         x = torch.randn((B, ld), generator=gen, device=dev, dtype=torch.float32).mul_(3.0)
         pool.append(x.to(tdt))
         del x
-    from neuralsteganography_amd.dist import reduce_job, shard_range
+    from neuralsteganography_amd.dist import per_rank, reduce_job, shard_range
 
     mine = shard_range(B * world, world, rank)  # weak scaling: B streams per rank, disjoint payload seeds
     payload_bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.payload_bytes)) for s in mine]
@@ -381,6 +383,7 @@ def main():
     pcie = None if args.no_pcie else host_logits_rate(args, sess, pool[0], stream)
 
     bits_all, ss_all, elapsed_max, kern_ms_max = reduce_job(bits, stream_steps, elapsed, kern_ms, device=dev)
+    rank_s = per_rank(elapsed, device=dev)
 
     from neuralsteganography_amd import _lib
 
@@ -400,6 +403,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed_max / args.steps,
+        "per_rank_seconds": rank_s,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -42,6 +42,20 @@ def reduce_job(bits: float, stream_steps: float, elapsed_s: float, kernel_ms: fl
     return float(s[0]), float(s[1]), float(m[0]), float(m[1])
 
 
+def per_rank(value: float, device=None) -> List[float]:
+    """``value`` of every rank, in rank order (per-GPU times expose load imbalance from the
+    variable number of tokens per stream)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    dev = device if device is not None else ("cuda" if dist.get_backend() == "nccl" else "cpu")
+    parts = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, torch.tensor([float(value)], dtype=torch.float64, device=dev))
+    return [float(p[0]) for p in parts]
+
+
 def gather_streams(local: Sequence, total: int) -> List:
     """Gather per-rank results (ordered by the shard of each rank) into one list of ``total`` items on
     every rank."""
@@ -70,4 +84,4 @@ def encode_sharded(provider, bit_lists: Sequence[Sequence[int]], context: Sequen
     return gather_streams(local, len(bit_lists))
 
 
-__all__ = ["world_info", "shard_range", "reduce_job", "gather_streams", "encode_sharded"]
+__all__ = ["world_info", "shard_range", "reduce_job", "per_rank", "gather_streams", "encode_sharded"]

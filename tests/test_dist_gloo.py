@@ -42,7 +42,7 @@ def _worker(rank, world, port, q):
         bits = [[(s >> k) & 1 for k in range(16)] for s in range(11)]
         toks = nd.encode_sharded(_EchoProvider(), bits, [1, 2, 3], quality={})
         b, ss, el, km = nd.reduce_job(100.0 * (rank + 1), 10.0, 1.0 + rank, 0.5 * (rank + 1))
-        q.put((rank, toks, (b, ss, el, km)))
+        q.put((rank, toks, (b, ss, el, km), nd.per_rank(1.5 * rank + 0.25)))
     finally:
         dist.destroy_process_group()
 
@@ -68,6 +68,7 @@ def test_world2_gloo_sharded_encode_and_reductions():
         assert p.exitcode == 0
     expect = _EchoProvider().encode_batch([[(s >> k) & 1 for k in range(16)] for s in range(11)], [1, 2, 3],
                                           quality={})
-    for rank, toks, red in res:
+    for rank, toks, red, times in res:
         assert toks == expect  # every rank sees all 11 streams, in stream order
         assert red == (300.0, 20.0, 2.0, 1.0)  # bits summed, stream-steps summed, times max
+        assert times == [0.25, 1.75]  # per-rank values in rank order on every rank
