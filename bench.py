@@ -72,13 +72,15 @@ def parse():
     return ap.parse_args()
 
 
-def _cpu_workers(module, argv, seconds):
-    """One child process per host core (the affinity mask, capped at the box's 16-CPU share), each running
-    ``python -m <module> <argv...>`` on one thread; returns (cores, parsed JSON results)."""
+def _cpu_workers(module, argv, seconds, max_workers=16):
+    """One child process per host core (the affinity mask, capped at the box's 16-CPU share and at
+    ``max_workers``), each running ``python -m <module> <argv...>`` on one thread with the GPU hidden; returns
+    (cores, parsed JSON results)."""
     import subprocess
 
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cores = max(1, min(16, max_workers, len(os.sched_getaffinity(0))))
+    env = dict(os.environ, OMP_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="",
+               CUDA_VISIBLE_DEVICES="")
     procs = []
     for c in range(cores):
         cmd = [sys.executable, "-m", module] + [str(a) for a in argv(c)]
@@ -113,7 +115,8 @@ def cpu_baseline(args, seconds, streams_per_core=16):
     if args.cpu_e2e_seconds > 0:
         cores, res = _cpu_workers("oracle.cpu_e2e", lambda c: [args.cpu_e2e_seconds, 2000 + c, args.vocab,
                                                                args.temp, args.precision, args.topk,
-                                                               args.payload_bytes], args.cpu_e2e_seconds)
+                                                               args.payload_bytes], args.cpu_e2e_seconds,
+                                  max_workers=8)  # torch workers: keep the box's GPU-process count bounded
         dt = max(r["seconds"] for r in res)
         bits = sum(r["bits"] for r in res)
         tok = sum(r["tokens"] for r in res)

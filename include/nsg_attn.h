@@ -7,8 +7,8 @@
  * GPT2Attention over the whole unbounded cache: softmax(q k^T / sqrt(D)) v).  It fuses the KV append of
  * the new token with the attention over the cache: one wavefront per (stream, head) streams the K and V rows
  * of that head once from HBM (online softmax in fp32), so the step is HBM-bound at B*(L+1)*2*D*2 bytes per
- * layer.  A pair's rows are split over 1, 2, 4 or 8 waves by the key count alone (one wave up to 128 keys, eight
- * beyond 512), partials merged in wave order: the summation order -- and every output bit -- does not depend on
+ * layer.  A pair's rows are split over 1, 2, 4 or 8 waves by the key count alone (one wave up to 256 keys, eight
+ * beyond 1,024), partials merged in wave order: the summation order -- and every output bit -- does not depend on
  * the batch size, so the decoder of a cover reproduces the encoder's logits at any B.  fp16 in and out, fp32
  * accumulation; no allocation, stream-ordered on the caller's hipStream_t.
  */

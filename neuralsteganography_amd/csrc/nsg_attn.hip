@@ -24,7 +24,7 @@
 namespace nsg {
 
 #ifndef NSG_ATT_ROWS1
-#define NSG_ATT_ROWS1 128  // keys per pair up to which one wave takes the whole pair (then 2, 4, 8 waves)
+#define NSG_ATT_ROWS1 256  // keys per pair up to which one wave takes the whole pair (then 2, 4, 8 waves)
 #endif
 #ifndef NSG_ATT_SMALL_PAIRS
 #define NSG_ATT_SMALL_PAIRS 1024  // up to this many (stream, head) pairs: one pair per workgroup

@@ -42,6 +42,12 @@
 #ifndef NSG_FMA_ARG
 #define NSG_FMA_ARG 1  // fast-sum exponent as one fma (x*c - r*c) with packed / two-chain fp32 sums
 #endif
+#ifndef NSG_ASM_APPEND
+#define NSG_ASM_APPEND 0
+#endif
+#ifndef NSG_DIAG_NOWRITE
+#define NSG_DIAG_NOWRITE 0
+#endif
 #ifndef NSG_BUCKET_CAP
 #define NSG_BUCKET_CAP 48  // largest bucket the bucket rank accepts (its fix-up loop runs that often)
 #endif
@@ -306,6 +312,33 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
         return;
     }
     int pos = c.cnt + excl;
+#if NSG_DIAG_NOWRITE  // timing diagnostic only: count and prefix, no LDS writes, never compacts (wrong results)
+    (void)pos;
+    c.cnt = min(c.cnt + total, CAND / 2);
+    return;
+#endif
+#if NSG_ASM_APPEND
+    // branch-free appends: each slot's write is issued under exec = (lanes whose value passes); an empty mask
+    // makes it a no-op.  LDS ops of a wave complete in order, so the compiler's own lgkmcnt waits stay valid.
+    const uint32_t kb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t*)c.keys;
+#pragma unroll
+    for (int d = 0; d < G; ++d)
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            const bool pass = x[d][q] > c.thr;
+            const uint64_t m = ballot(pass);
+            const uint64_t e = raw_entry(x[d][q], (uint32_t)(jb + d * TS + q));
+            uint64_t saved;
+            asm volatile(
+                "s_and_saveexec_b64 %0, %1\n\t"
+                "ds_write_b64 %2, %3\n\t"
+                "s_mov_b64 exec, %0"
+                : "=&s"(saved)
+                : "s"(m), "v"(kb + 8u * (uint32_t)pos), "v"(e)
+                : "memory");
+            pos += pass ? 1 : 0;
+        }
+#else
 #pragma unroll
     for (int d = 0; d < G; ++d)
 #pragma unroll
@@ -314,6 +347,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
                 c.keys[pos] = raw_entry(x[d][q], (uint32_t)(jb + d * TS + q));
                 ++pos;
             }
+#endif
     c.cnt += total;
 }
 
