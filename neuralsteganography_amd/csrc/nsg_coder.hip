@@ -1200,7 +1200,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.9 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.10 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
