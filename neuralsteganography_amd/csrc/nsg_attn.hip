@@ -315,7 +315,11 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
             for (int h8 = 0; h8 < DPL / 8; ++h8) {
                 f16x8 o;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = (_Float16)(acc[h8 * 8 + i] * inv);
+                for (int i = 0; i < 8; ++i) {
+                    float t = acc[h8 * 8 + i] * inv;
+                    asm volatile("" : "+v"(t));  // no fused multiply-convert (one rounding) in some variants only
+                    o[i] = (_Float16)t;
+                }
                 *(f16x8*)(out + (int64_t)b * out_stride + h * ATT_D + c * DPL + h8 * 8) = o;
             }
         }

@@ -51,6 +51,14 @@ __device__ __forceinline__ float gelu_tanh(float x) {
     return 0.5f * x * (1.0f + tanhf(u));
 }
 
+// fp32 -> fp16 with the fp32 value pinned first: without the barrier the compiler may fold the producing
+// multiply / add into the conversion (v_fma_mix*_f16: ONE rounding to fp16 instead of fp32 then fp16), and it
+// does so in some kernel variants and not in others -- the tile configurations must give the same bits.
+__device__ __forceinline__ f16 to_f16(float v) {
+    asm volatile("" : "+v"(v));
+    return (f16)v;
+}
+
 // Epilogue of one 16x16 fragment: lane holds n0..n0+3 of row m.
 template <int EPI>
 __device__ __forceinline__ void store4(void* Y, int64_t ldy, const f16* __restrict__ bias, int m, int n, f32x4 acc) {
@@ -72,13 +80,41 @@ __device__ __forceinline__ void store4(void* Y, int64_t ldy, const f16* __restri
         if constexpr (EPI == NS_LM_EPI_RESIDUAL) {
             const f16x4 h = *(const f16x4*)y;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)((float)h[r] + v[r]);
+            for (int r = 0; r < 4; ++r) o[r] = to_f16((float)h[r] + v[r]);
         } else if constexpr (EPI == NS_LM_EPI_GELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)gelu_tanh(v[r]);
+            for (int r = 0; r < 4; ++r) o[r] = to_f16(gelu_tanh(v[r]));
         } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+            for (int r = 0; r < 4; ++r) o[r] = to_f16(v[r]);
+        }
+        *(f16x4*)y = o;
+    }
+}
+
+// The same epilogue with its operands (bias, residual) loaded ahead: small-batch kernels issue those loads before
+// the K loop, so they land during it instead of costing one more dependent memory round trip at the end.
+template <int EPI>
+__device__ __forceinline__ void store4_pre(void* Y, int64_t ldy, bool has_bias, f16x4 bb, f16x4 h, int m, int n,
+                                           f32x4 acc) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = has_bias ? acc[r] + (float)bb[r] : acc[r];
+    if constexpr (EPI == NS_LM_EPI_STORE_F32) {
+        float* y = (float*)Y + (int64_t)m * ldy + n;
+        *(f32x4*)y = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+        f16* y = (f16*)Y + (int64_t)m * ldy + n;
+        f16x4 o;
+        if constexpr (EPI == NS_LM_EPI_RESIDUAL) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = to_f16((float)h[r] + v[r]);
+        } else if constexpr (EPI == NS_LM_EPI_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = to_f16(gelu_tanh(v[r]));
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = to_f16(v[r]);
         }
         *(f16x4*)y = o;
     }
@@ -117,6 +153,22 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
     f32x4 acc[FM];
 #pragma unroll
     for (int f = 0; f < FM; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // epilogue operands first (bias, the residual row): in flight with the K loop's loads
+    const int n = nb * 16 + 4 * c;
+    const bool ep = live && n < N && (SK == 1 || chain == 0);
+    f16x4 pb = {}, ph[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) ph[f] = f16x4{};
+    if (ep) {
+        if (bias) pb = *(const f16x4*)(bias + n);
+        if constexpr (EPI == NS_LM_EPI_RESIDUAL) {
+#pragma unroll
+            for (int f = 0; f < FM; ++f) {
+                const int m = m0 + f * 16 + r;
+                if (m < M) ph[f] = *(const f16x4*)((const f16*)Y + (int64_t)m * ldy + n);
+            }
+        }
+    }
     constexpr int U = FM == 1 ? 24 : FM == 2 ? 12 : 8;  // 32-wide k-steps per batch of loads in flight (K = 768: one)
     int k = k_begin;
     if (live) {
@@ -151,12 +203,11 @@ __global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, in
 #pragma unroll
             for (int f = 0; f < FM; ++f) acc[f] += s_part[wave + q][f][lane];
     }
-    const int n = nb * 16 + 4 * c;
-    if (!live || n >= N) return;
+    if (!ep) return;
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
         const int m = m0 + f * 16 + r;
-        if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[f]);
+        if (m < M) store4_pre<EPI>(Y, ldy, bias != nullptr, pb, ph[f], m, n, acc[f]);
     }
 }
 
@@ -348,6 +399,16 @@ __device__ __forceinline__ float wave_sum(float s) {
 __device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, const f16* __restrict__ w,
                                        const f16* __restrict__ b, f16* __restrict__ y, float eps) {
     const int lane = threadIdx.x & 63;
+    // the affine parameters do not depend on the row: load them before the reductions (one round trip, not two)
+    f16x4 wv[LN_MAXV], bv[LN_MAXV];
+#pragma unroll
+    for (int v = 0; v < LN_MAXV; ++v) {
+        const int i = lane + 64 * v;
+        if (i < NV4) {
+            wv[v] = *(const f16x4*)(w + 4 * i);
+            bv[v] = *(const f16x4*)(b + 4 * i);
+        }
+    }
     float s = 0.0f;
 #pragma unroll
     for (int v = 0; v < LN_MAXV; ++v)
@@ -370,11 +431,9 @@ __device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, c
     for (int v = 0; v < LN_MAXV; ++v) {
         const int i = lane + 64 * v;
         if (i < NV4) {
-            const f16x4 ww = *(const f16x4*)(w + 4 * i);
-            const f16x4 bb = *(const f16x4*)(b + 4 * i);
             f16x4 o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (f16)(((x[v][e] - mean) * rstd) * (float)ww[e] + (float)bb[e]);
+            for (int e = 0; e < 4; ++e) o[e] = (f16)(((x[v][e] - mean) * rstd) * (float)wv[v][e] + (float)bv[v][e]);
             *(f16x4*)(y + 4 * i) = o;
         }
     }
