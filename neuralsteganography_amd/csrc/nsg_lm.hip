@@ -433,7 +433,7 @@ __device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, c
         if (i < NV4) {
             f16x4 o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (f16)(((x[v][e] - mean) * rstd) * (float)wv[v][e] + (float)bv[v][e]);
+            for (int e = 0; e < 4; ++e) o[e] = to_f16(((x[v][e] - mean) * rstd) * (float)wv[v][e] + (float)bv[v][e]);
             *(f16x4*)(y + 4 * i) = o;
         }
     }
