@@ -37,7 +37,7 @@
 #include "nsg_host.h"
 
 #ifndef NSG_SAMPLE
-#define NSG_SAMPLE 16  // stratified sample: this many 64-id blocks (values per lane) for the speculative threshold
+#define NSG_SAMPLE 64  // sample size / 64 ids: whole tiles spread over the row (16 fp32 / 8 fp16 tiles)
 #endif
 #ifndef NSG_FMA_ARG
 #define NSG_FMA_ARG 1  // fast-sum exponent as one fma (x*c - r*c) with packed / two-chain fp32 sums
@@ -244,6 +244,14 @@ __device__ __forceinline__ void to_keys(Cand& c, int lane) {
     lds_fence();
 }
 
+// A threshold t with x > t for every x whose value is >= v in key order (-inf stays -inf: never admitted).
+// The next float below v, or -FLT_MIN around zero (+0 > -0 is false; denormals may flush).
+__device__ __forceinline__ float thr_below(float v) {
+    if (!(v > -__builtin_inff())) return v;
+    const float t = unord32(ord32(v) - 1u);
+    return t < v ? t : -1.17549435e-38f;
+}
+
 template <int W>
 __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int K, int lane) {
     float mx = x[0];
@@ -262,8 +270,9 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
         const uint64_t kappa = compact_topk(c.keys, c.scr, c.cnt, K, lane);
         ++c.ncompact;
         c.cnt = c.conv = K;
-        // later elements have larger ids than every buffered key, so ties at the K-th value rank below it
-        c.thr = key_val(kappa);
+        // admit ties at the K-th value: the sample tiles are offered before the stream, so a later element can
+        // carry a smaller id than the K-th key (a superset is always safe; the final selection is exact)
+        c.thr = thr_below(key_val(kappa));
         npt = 0;
 #pragma unroll
         for (int q = 0; q < W; ++q) {
@@ -294,10 +303,12 @@ __device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
 
 // Group form of offer(): G tiles (G*W values per lane) share one reject test, one wave prefix and one
 // capacity check; passing values are written with predicated stores at lane-private positions.  If the
-// group does not fit, the per-tile path (which compacts as needed and always fits) takes over.
+// group does not fit, the per-tile path (which compacts as needed and always fits) takes over.  Tile d's
+// value q of this lane has id tb[d] + lj + q: tb[d] the tile's first id (wave-uniform; the tiles of a group
+// need not be adjacent), lj = lane * W.
 template <int W, int G>
-__device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int jb, int K, int lane) {
-    constexpr int TS = WAVE * W;
+__device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], const int (&tb)[G], int lj, int K,
+                                            int lane) {
     int n = 0;
 #pragma unroll
     for (int d = 0; d < G; ++d)
@@ -308,7 +319,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
     if (total == 0) return;
     if (c.cnt + total > CAND) {
 #pragma unroll
-        for (int d = 0; d < G; ++d) offer<W>(c, x[d], jb + d * TS, K, lane);
+        for (int d = 0; d < G; ++d) offer<W>(c, x[d], tb[d] + lj, K, lane);
         return;
     }
     int pos = c.cnt + excl;
@@ -327,7 +338,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
         for (int q = 0; q < W; ++q) {
             const bool pass = x[d][q] > c.thr;
             const uint64_t m = ballot(pass);
-            const uint64_t e = raw_entry(x[d][q], (uint32_t)(jb + d * TS + q));
+            const uint64_t e = raw_entry(x[d][q], (uint32_t)(tb[d] + lj + q));
             uint64_t saved;
             asm volatile(
                 "s_and_saveexec_b64 %0, %1\n\t"
@@ -344,7 +355,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], int
 #pragma unroll
         for (int q = 0; q < W; ++q)
             if (x[d][q] > c.thr) {
-                c.keys[pos] = raw_entry(x[d][q], (uint32_t)(jb + d * TS + q));
+                c.keys[pos] = raw_entry(x[d][q], (uint32_t)(tb[d] + lj + q));
                 ++pos;
             }
 #endif
@@ -594,41 +605,83 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     cand.thr = -__builtin_inff();
     int nfallback = 0;
 
-    // the streaming ring's first tiles go out before the sample: they land while the threshold is computed
+    // ---------------- stream order ----------------
+    // With a sample (p.spec_j > 0) NSAMP whole tiles spread over the row -- tile s*space + space-1, 4,096 ids --
+    // are read first and give r and the speculative threshold.  The last NKEEP of them stay in registers and
+    // are accumulated and offered like any other tile; the stream visits every other tile in increasing order,
+    // the first NSAMP - NKEEP sample tiles included (fp32 rows: keeping all 16 would spill; those 8 KiB are read
+    // again, with the default cache policy on their first read).  The host enables the sample only when
+    // ntiles >= 2*NSAMP (space >= 2).
+    constexpr int NSAMP = (64 * NSG_SAMPLE) / TS;
+    constexpr int NKEEP = NSAMP < 8 ? NSAMP : 8;
+    constexpr int S0 = NSAMP - NKEEP;  // first kept sample tile
+    static_assert(NKEEP >= PREFETCH && NKEEP % PREFETCH == 0, "kept sample tiles come in ring-sized groups");
+    const bool spec_on = p.spec_j > 0;
+    const int space = spec_on ? ntiles / NSAMP : 1;
+    const int nstream = spec_on ? ntiles - NKEEP : ntiles;
+    // load cursor (wave-uniform): next tile to load, non-skipped tiles left before the next kept sample tile
+    int lt = 0, lc = spec_on ? S0 * space + space - 1 : 0x7FFFFFFF, sleft = spec_on ? NKEEP : 0;
+    auto next_tile = [&]() -> int {
+        const int t = lt++;
+        if (--lc == 0) {  // reaches 0 only while kept sample tiles remain: skip one
+            ++lt;
+            lc = --sleft > 0 ? space - 1 : 0x7FFFFFFF;
+        }
+        return t;
+    };
+    // the streaming ring: without a sample its first tiles go out now; with one, once the first sample group has
+    // been consumed (the registers it frees hold the ring)
     uint4 buf[PREFETCH];
+    int tid[PREFETCH];
+    auto issue_ring = [&]() {
 #pragma unroll
-    for (int d = 0; d < PREFETCH; ++d) buf[d] = rd.vec(d * WAVE + lane);
+        for (int d = 0; d < PREFETCH; ++d) {
+            tid[d] = next_tile();
+            buf[d] = rd.vec(tid[d] * WAVE + lane);
+        }
+    };
+    if (!spec_on) issue_ring();
 
-    // ---------------- prologue: stratified sample -> softmax reference r and speculative threshold -----
-    // 16 blocks of 64 ids spread over the row (16 values per lane).  r = sample max (fast-sum reference);
-    // thr = the spec_j-th largest sample value (16-bit prefix), a GUESS verified at the end of the row.
+    // ---------------- prologue: sample tiles -> softmax reference r and speculative threshold -----
+    // r = sample max (fast-sum reference); thr = a lower bound of the spec_j-th largest sample value (16-bit
+    // prefix), a GUESS verified at the end of the row.  The count runs over each lane's three largest sample
+    // values only (4,096 values, ~J/64 per lane above the answer): it can only undercount, which lowers the
+    // threshold -- more appends, never a wrong result.
     float r = 0.0f;
     bool spec = false;
-    if (p.spec_j > 0) {
-        constexpr int NS = NSG_SAMPLE;  // sample values per lane = 64-id blocks
-        constexpr int LPB = WAVE / W;   // lanes per 64-id block
-        constexpr int NLD = NS / W;     // sample loads per lane
-        float sv[NS];
+    uint4 smp[NKEEP];  // the kept sample tiles as loaded (fp16 stays packed)
+    if (spec_on) {
+        uint4 sx[S0 > 0 ? S0 : 1];
 #pragma unroll
-        for (int i = 0; i < NLD; ++i) {
-            const int blk = i * W + lane / LPB;
-            const int jb = ((int)(((int64_t)blk * V) / NS) / W) * W + (lane % LPB) * W;
-            float x[W];
-            Elem<T>::unpack(rd.vec(jb / W), x);
-#pragma unroll
-            for (int q = 0; q < W; ++q) sv[i * W + q] = is_banned(p, jb + q) ? -__builtin_inff() : x[q];
+        for (int s = 0; s < NSAMP; ++s) {
+            const int v = (s * space + space - 1) * WAVE + lane;
+            if (s < S0) sx[min(s, S0 > 0 ? S0 - 1 : 0)] = rd.vec_keep(v); else smp[max(s - S0, 0)] = rd.vec(v);
         }
-        float mx = sv[0];
+        int sbi = 0, snb = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        float t0 = -__builtin_inff(), t1 = -__builtin_inff(), t2 = -__builtin_inff();
 #pragma unroll
-        for (int i = 1; i < NS; ++i) mx = fmaxf(mx, sv[i]);
-        r = wave_max(mx);
+        for (int s = 0; s < NSAMP; ++s) {
+            const int ts = s * space + space - 1;
+            float x[W];
+            Elem<T>::unpack(s < S0 ? sx[min(s, S0 > 0 ? S0 - 1 : 0)] : smp[max(s - S0, 0)], x);
+            mask_tile<W>(p, x, ts, ntiles, ts * TS + lane * W, sbi, snb);
+#pragma unroll
+            for (int q = 0; q < W; ++q) {  // per-lane top 3
+                const float v = x[q];
+                const float a = fminf(t0, v);
+                t0 = fmaxf(t0, v);
+                const float c = fminf(t1, a);
+                t1 = fmaxf(t1, a);
+                t2 = fmaxf(t2, c);
+            }
+        }
+        r = wave_max(t0);
         if (r == -__builtin_inff()) r = 0.0f;
+        const uint32_t o0 = ord32(t0), o1 = ord32(t1), o2 = ord32(t2);
         uint32_t pre = 0;
         for (int bit = 31; bit >= 16; --bit) {
             const uint32_t c = pre | (1u << bit);
-            int n = 0;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) n += popc64(ballot(ord32(sv[i]) >= c));
+            const int n = popc64(ballot(o0 >= c)) + popc64(ballot(o1 >= c)) + popc64(ballot(o2 >= c));
             if (n >= p.spec_j) pre = c;
         }
         if (pre > 0x00800000u) {  // above ord(-inf): a finite threshold
@@ -706,31 +759,53 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         accumulate(x, W);
         offer<W>(cand, x, j0, K, lane);
     };
-    // Full groups: every slot is consumed, then refilled PREFETCH tiles ahead into the same registers
-    // (no copies, so the per-tile wait is a counted vmcnt, never a drain).  Loads past the row are
+    // The kept sample tiles first (still in registers), in ring-sized groups; then the ring goes out.
+    if (spec_on) {
+        int sbi = 0, snb = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+#pragma unroll
+        for (int g = 0; g < NKEEP; g += PREFETCH) {
+            float xg[PREFETCH][W];
+            int tb[PREFETCH];
+#pragma unroll
+            for (int d = 0; d < PREFETCH; ++d) {
+                const int ts = (S0 + g + d) * space + space - 1;
+                tb[d] = ts * TS;
+                Elem<T>::unpack(smp[g + d], xg[d]);
+                mask_tile<W>(p, xg[d], ts, ntiles, tb[d] + lane * W, sbi, snb);
+            }
+            accumulate(&xg[0][0], PREFETCH * W);
+            offer_group<W, PREFETCH>(cand, xg, tb, lane * W, K, lane);
+        }
+        issue_ring();
+    }
+    // Full groups: every slot is consumed, then refilled PREFETCH stream positions ahead into the same
+    // registers (no copies, so the per-tile wait is a counted vmcnt, never a drain).  Loads past the row are
     // range-checked by the buffer descriptor and return zeros.
-    int tile = 0;
-    for (; tile + PREFETCH <= ntiles; tile += PREFETCH) {
+    int pos = 0;
+    for (; pos + PREFETCH <= nstream; pos += PREFETCH) {
         float xg[PREFETCH][W];
+        int jt[PREFETCH], tb[PREFETCH];
 #pragma unroll
         for (int d = 0; d < PREFETCH; ++d) {
             Elem<T>::unpack(buf[d], xg[d]);
-            buf[d] = rd.vec((tile + d + PREFETCH) * WAVE + lane);
+            jt[d] = tid[d];
+            tb[d] = jt[d] * TS;
+            tid[d] = next_tile();
+            buf[d] = rd.vec(tid[d] * WAVE + lane);
         }
-        const int jb = (tile * WAVE + lane) * W;  // id of xg[d][q] = jb + d*TS + q
-        if (tile + PREFETCH == ntiles || next_ban < (tile + PREFETCH) * TS) {  // rare: tail or banned id
+        if (jt[PREFETCH - 1] == ntiles - 1 || next_ban < (jt[PREFETCH - 1] + 1) * TS) {  // rare: tail or banned id
 #pragma unroll
-            for (int d = 0; d < PREFETCH; ++d) mask_tile<W>(p, xg[d], tile + d, ntiles, jb + d * TS, bi, next_ban);
+            for (int d = 0; d < PREFETCH; ++d) mask_tile<W>(p, xg[d], jt[d], ntiles, tb[d] + lane * W, bi, next_ban);
         }
         accumulate(&xg[0][0], PREFETCH * W);
-        offer_group<W, PREFETCH>(cand, xg, jb, K, lane);
+        offer_group<W, PREFETCH>(cand, xg, tb, lane * W, K, lane);
     }
 #pragma unroll
     for (int d = 0; d < PREFETCH; ++d) {
-        if (tile + d < ntiles) {
+        if (pos + d < nstream) {
             float x[W];
             Elem<T>::unpack(buf[d], x);
-            process(x, tile + d);
+            process(x, tid[d]);
         }
     }
     NSG_STAMP(p, b, lane, 2);
@@ -1200,7 +1275,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.10 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.11 gfx950"; }
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
@@ -1307,16 +1382,18 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
     p.nbanned = nb;
     for (int i = 0; i < nb; ++i) p.banned[i] = ban[i];
     p.flags = flags;
-    // speculative candidate threshold: the spec_j-th largest of a 64*NSG_SAMPLE-id stratified sample.  The number
-    // of sample ids above the row's true K-th key is ~Poisson(lambda = 64*NSG_SAMPLE*K / nvalid); spec_j is the smallest j
-    // with P(Poisson(lambda) >= j) <= 1e-6, so a miss (one extra row read by that wave) stays a rare event
-    // for every K.  NSG_SPEC_FACTOR (tuning override) instead sets spec_j = factor * lambda + 1.
+    // speculative candidate threshold: the spec_j-th largest of a 64*NSG_SAMPLE-id stratified sample (whole tiles
+    // spread over the row; the kernel needs at least two sample spacings, hence vocab >= 2 * 64*NSG_SAMPLE).  The
+    // number of sample ids above the row's true K-th key is ~Poisson(lambda = 64*NSG_SAMPLE*K / nvalid); spec_j is
+    // the smallest j with P(Poisson(lambda) >= j) <= 1e-6, so a miss (one extra row read by that wave) stays a rare
+    // event for every K.  The kernel counts each lane's three largest sample values, so spec_j stays well below
+    // 3*64.  NSG_SPEC_FACTOR (tuning override) instead sets spec_j = factor * lambda + 1.
     p.spec_j = 0;
     static const double spec_factor = [] {
         const char* e = getenv("NSG_SPEC_FACTOR");
         return e ? atof(e) : 0.0;
     }();
-    if (ctx->vocab >= 2048) {
+    if (ctx->vocab >= 2 * 64 * NSG_SAMPLE) {
         const double lambda = (double)K * (64.0 * NSG_SAMPLE) / (double)nvalid;
         int sj;
         if (spec_factor > 0.0) {
@@ -1331,7 +1408,7 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
             }
         }
         if (sj < 4) sj = 4;
-        if (sj < 256) p.spec_j = sj;
+        if (sj <= 160) p.spec_j = sj;
     }
     p.state = d_state;
     p.trace = d_trace;

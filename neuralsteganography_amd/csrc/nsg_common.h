@@ -232,7 +232,7 @@ struct StepParams {
     float c32;  // (float)(inv_temp * log2(e))
     int nbanned;
     int banned[NS_MAX_BANNED];  // sorted ascending, unique, in [0, V)
-    int spec_j;  // speculative threshold rank in the 1024-id sample (0: no sample)
+    int spec_j;  // speculative threshold rank in the 4096-id sample (0: no sample)
     uint32_t flags;
     // encode
     const uint8_t* payload;

@@ -224,10 +224,16 @@ def test_empty_and_single_bit_payloads():
 
 
 def _sample_ids(V, W=4):
+    """Ids of the kernel's sample tiles (nsg_coder.hip, NSG_SAMPLE 64): 4,096 ids as whole 64*W-id tiles,
+    tile s*space + space-1 for s < NSAMP, space = ntiles // NSAMP."""
+    ts = 64 * W
+    nsamp = 4096 // ts
+    ntiles = (V + ts - 1) // ts
+    space = ntiles // nsamp
     ids = []
-    for blk in range(16):
-        start = ((blk * V) // 16) // W * W
-        ids.extend(range(start, start + 64))
+    for s in range(nsamp):
+        t = s * space + space - 1
+        ids.extend(range(t * ts, min((t + 1) * ts, V)))
     return np.asarray(ids)
 
 
@@ -277,6 +283,54 @@ def test_adversarial_rows_exercise_fallback_paths(mode):
         assert c1[1] > c0[1], "overflow compaction path was not exercised"
     else:
         assert c1[3] > c0[3], "slow top-K selection path was not exercised"
+
+
+def test_sample_tie_rows_admit_smaller_ids():
+    """The sample tiles are offered before the stream.  Rows with one top value, held by half of the sample
+    tiles' ids and 3 % of the others: the sample alone overflows the candidate buffer, and the compaction's K-th
+    key then sits in a sample tile while the stream's EARLIER tiles hold ids of the same value with smaller ids
+    -- they rank above it and must still be admitted (a strict x > K-th-value rule drops them).  Token by token against the oracle for a fixed number of
+    steps (the reference's interval can stall at the midpoint on such flat rows, so runs are not taken to
+    completion)."""
+    from neuralsteganography_amd.coder import CoderParams, EncodeSession, row_stride
+
+    torch = _torch()
+    V, B, T = 50257, 4, 12
+    params = CoderParams(vocab=V, precision=26, temp=0.9, topk=300)
+    ctx = _ctx(params, B)
+    ld = row_stride(V, "f32")
+    samp = _sample_ids(V)
+
+    def row(s, t):  # one top value: the top-K is the K smallest ids holding it
+        u = np.random.default_rng([77, s, t]).random(V)
+        x = np.where(u < 0.03, 2.0, 0.0)
+        x[samp] = np.where(u[samp] < 0.5, 2.0, 0.0)
+        return x.astype(np.float32)
+
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 8)) for s in range(B)]
+    expect = []
+    for s in range(B):
+        packed = np.packbits(np.asarray(bits[s], dtype=np.uint8), bitorder="little")
+        st = oracle.new_state(26)
+        toks = []
+        for t in range(T):
+            if st.bit_pos >= len(bits[s]):
+                break
+            rc, tok, _ = oracle.encode_step(row(s, t), st, packed, len(bits[s]), banned=params.banned_ids(),
+                                            temp=0.9, precision=26, topk=300)
+            assert rc == oracle.OR_OK
+            toks.append(tok)
+        expect.append(toks)
+    sess = EncodeSession(ctx, bits)
+    c0 = ctx.counters()
+    for t in range(T):
+        arr = np.zeros((B, ld), np.float32)
+        for s in range(B):
+            arr[s, :V] = row(s, t)
+        sess.step(torch.from_numpy(arr).cuda())
+    c1 = ctx.counters()
+    assert sess.tokens() == expect
+    assert c1[1] > c0[1], "overflow compaction path was not exercised"
 
 
 @pytest.mark.parametrize("mode,dtype", [("plain", "f32"), ("ties", "f32"), ("outlier", "f32"), ("mixed", "f32"),
