@@ -96,6 +96,11 @@ const char* ns_version(void);
 /* Largest topk the single-pass kernel handles for a logits dtype (larger topk takes the wide path). */
 int ns_max_topk(int logits_dtype);
 
+/* Single-pass steps of at most `max_batch` streams run the split form (one workgroup of 16 fp32 / 8 fp16 waves per
+ * stream) instead of one wave per stream; 0 disables it.  Default 256 (environment NSG_SPLIT_MAX_B).  Process-wide;
+ * speed only -- both forms emit the same tokens and bits.  Returns the previous value. */
+int ns_set_split_max_batch(int max_batch);
+
 /* Reset B stream states to [0, 2^precision), bit_pos 0. */
 int ns_init_state(ns_ctx* ctx, ns_stream_state* d_state, int B, void* hip_stream);
 

@@ -25,7 +25,8 @@ NS_STEP_FINISH_SENT = 16
 NS_STEP_DIAG_STREAM_ONLY, NS_STEP_DIAG_NO_CANDIDATES, NS_STEP_DIAG_SKIP_CDF = 2, 4, 8
 NS_MAX_BANNED = 8
 
-EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_init_state",
+EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_set_split_max_batch",
+           "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
@@ -140,6 +141,8 @@ def lib() -> ctypes.CDLL:
     L.ns_lm_gemm_configs.argtypes = []
     L.ns_lm_layernorm.restype = ci
     L.ns_lm_layernorm.argtypes = [vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_set_split_max_batch.restype = ci
+    L.ns_set_split_max_batch.argtypes = [ci]
     L.ns_lm_embed_ln.restype = ci
     L.ns_lm_embed_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
     _lib = L
@@ -148,6 +151,12 @@ def lib() -> ctypes.CDLL:
 
 def version() -> str:
     return lib().ns_version().decode()
+
+
+def set_split_max_batch(max_batch: int) -> int:
+    """Steps of at most max_batch streams use the split (workgroup-per-stream) coder form; returns the previous
+    limit.  Speed only: both forms give the same tokens and bits."""
+    return int(lib().ns_set_split_max_batch(int(max_batch)))
 
 
 def max_topk(dtype_code: int) -> int:

@@ -560,17 +560,25 @@ __device__ __forceinline__ void sample_tail(const StepParams& p, int b, const ns
     }
 }
 
-template <typename T, bool DECODE, int NSK, bool STATS>
-__global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_kernel(StepParams p) {
+// NSPLIT = 1: one wave per stream, WPB streams per workgroup.  NSPLIT > 1 (small batches, round 2): one workgroup
+// of NSPLIT = NSAMP waves per stream; wave w streams the w-th slice of the row (its sample tile is the slice's
+// last tile), the waves agree on r and the threshold through LDS, and wave 0 merges the candidate buffers and
+// fast-sum partials and runs the tail alone.  The emitted integers are the same either way (the top-K keys are
+// exact and the cutoff decision is proven; tested bit-exact against the oracle in both forms).
+template <typename T, bool DECODE, int NSK, bool STATS, int NSPLIT = 1>
+__global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_kernel(StepParams p) {
     constexpr int W = Elem<T>::W;
     constexpr int TS = WAVE * W;  // elements per tile (one 16-byte load per lane)
     static_assert(NSK * WAVE <= CAND - TS, "K must leave room for one tile of appends");
-    __shared__ uint64_t s_keys[WPB][CAND];
-    __shared__ __attribute__((aligned(16))) uint32_t s_scr[WPB][SCR_U32];
+    constexpr int NWG = NSPLIT > 1 ? NSPLIT : WPB;  // waves per workgroup
+    __shared__ uint64_t s_keys[NWG][CAND];
+    __shared__ __attribute__((aligned(16))) uint32_t s_scr[NWG][SCR_U32];
+    __shared__ double s_part[NSPLIT > 1 ? NSPLIT : 1][3];  // split: per-wave fast-sum partials
+    __shared__ int s_cnt[NSPLIT > 1 ? NSPLIT : 1][3];      // split: cnt, conv, ncompact
 
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-    const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + wv);
+    const int b = __builtin_amdgcn_readfirstlane(NSPLIT > 1 ? (int)blockIdx.x : (int)blockIdx.x * WPB + wv);
     if (b >= p.B) return;
 
     NSG_STAMP_RT(p, b, lane, 9);
@@ -616,11 +624,17 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     constexpr int NKEEP = NSAMP < 8 ? NSAMP : 8;
     constexpr int S0 = NSAMP - NKEEP;  // first kept sample tile
     static_assert(NKEEP >= PREFETCH && NKEEP % PREFETCH == 0, "kept sample tiles come in ring-sized groups");
-    const bool spec_on = p.spec_j > 0;
+    static_assert(NSPLIT == 1 || NSPLIT == NSAMP, "split: one wave per sample tile");
+    const bool spec_on = p.spec_j > 0;  // always on in the split form (host)
     const int space = spec_on ? ntiles / NSAMP : 1;
-    const int nstream = spec_on ? ntiles - NKEEP : ntiles;
+    // split: wave w streams tiles [w*space, end) minus its sample tile w*space + space-1; the last wave takes the rest
+    const int nstream = !spec_on ? ntiles
+                        : NSPLIT > 1 ? (wv == NSPLIT - 1 ? ntiles : (wv + 1) * space) - wv * space - 1
+                                     : ntiles - NKEEP;
     // load cursor (wave-uniform): next tile to load, non-skipped tiles left before the next kept sample tile
-    int lt = 0, lc = spec_on ? S0 * space + space - 1 : 0x7FFFFFFF, sleft = spec_on ? NKEEP : 0;
+    int lt = NSPLIT > 1 ? wv * space : 0;
+    int lc = !spec_on ? 0x7FFFFFFF : NSPLIT > 1 ? space - 1 : S0 * space + space - 1;
+    int sleft = !spec_on ? 0 : NSPLIT > 1 ? 1 : NKEEP;
     auto next_tile = [&]() -> int {
         const int t = lt++;
         if (--lc == 0) {  // reaches 0 only while kept sample tiles remain: skip one
@@ -650,7 +664,52 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
     float r = 0.0f;
     bool spec = false;
     uint4 smp[NKEEP];  // the kept sample tiles as loaded (fp16 stays packed)
-    if (spec_on) {
+    if constexpr (NSPLIT > 1) {
+        // wave w reads sample tile w (its slice's last tile), then its ring; per-lane top 3 of the tile goes
+        // through LDS, and every wave derives the same r and threshold from the union (the same values as the
+        // one-wave form: the top 3 of the per-tile top 3s are the top 3 of all 4,096 values of the lane)
+        const int ts = wv * space + space - 1;
+        smp[0] = rd.vec(ts * WAVE + lane);
+        issue_ring();
+        float x[W];
+        Elem<T>::unpack(smp[0], x);
+        int sbi = 0, snb = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        mask_tile<W>(p, x, ts, ntiles, ts * TS + lane * W, sbi, snb);
+        uint32_t u0 = 0u, u1 = 0u, u2 = 0u;  // ord32 order; 0 is below every float
+        auto top3 = [&](uint32_t v) {
+            const uint32_t a = min(u0, v);
+            u0 = max(u0, v);
+            const uint32_t c = min(u1, a);
+            u1 = max(u1, a);
+            u2 = max(u2, c);
+        };
+#pragma unroll
+        for (int q = 0; q < W; ++q) top3(ord32(x[q]));
+        s_scr[wv][lane] = u0;
+        s_scr[wv][WAVE + lane] = u1;
+        s_scr[wv][2 * WAVE + lane] = u2;
+        __syncthreads();
+        u0 = u1 = u2 = 0u;
+#pragma unroll
+        for (int v = 0; v < NSPLIT; ++v) {
+            top3(s_scr[v][lane]);
+            top3(s_scr[v][WAVE + lane]);
+            top3(s_scr[v][2 * WAVE + lane]);
+        }
+        __syncthreads();  // every wave has read the exchange area before any scratch is reused
+        r = wave_max(unord32(u0));
+        if (r == -__builtin_inff()) r = 0.0f;
+        uint32_t pre = 0;
+        for (int bit = 31; bit >= 16; --bit) {
+            const uint32_t c = pre | (1u << bit);
+            const int n = popc64(ballot(u0 >= c)) + popc64(ballot(u1 >= c)) + popc64(ballot(u2 >= c));
+            if (n >= p.spec_j) pre = c;
+        }
+        if (pre > 0x00800000u) {
+            cand.thr = unord32(pre - 1u);
+            spec = true;
+        }
+    } else if (spec_on) {
         uint4 sx[S0 > 0 ? S0 : 1];
 #pragma unroll
         for (int s = 0; s < NSAMP; ++s) {
@@ -760,7 +819,15 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         offer<W>(cand, x, j0, K, lane);
     };
     // The kept sample tiles first (still in registers), in ring-sized groups; then the ring goes out.
-    if (spec_on) {
+    if constexpr (NSPLIT > 1) {
+        const int ts = wv * space + space - 1;
+        float x[W];
+        Elem<T>::unpack(smp[0], x);
+        int sbi = 0, snb = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+        mask_tile<W>(p, x, ts, ntiles, ts * TS + lane * W, sbi, snb);
+        accumulate(x, W);
+        offer<W>(cand, x, ts * TS + lane * W, K, lane);
+    } else if (spec_on) {
         int sbi = 0, snb = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
 #pragma unroll
         for (int g = 0; g < NKEEP; g += PREFETCH) {
@@ -809,6 +876,53 @@ __global__ __launch_bounds__(WPB* WAVE, NSG_MIN_WAVES_PER_EU) void coder_step_ke
         }
     }
     NSG_STAMP(p, b, lane, 2);
+    if constexpr (NSPLIT > 1) {
+        // hand the slice results to wave 0: fast-sum partials (reduced per wave, added in wave order) and the
+        // candidate buffers (copied into wave 0's, converted to keys; compacted to the top-K when full)
+        const double sa = wave_sum_butterfly(acc64);
+        const double sb = STATS ? wave_sum_butterfly(b64) : 0.0;
+        const double su = STATS ? wave_sum_butterfly(u64) : 0.0;
+        if (lane == 0) {
+            s_part[wv][0] = sa;
+            s_part[wv][1] = sb;
+            s_part[wv][2] = su;
+            s_cnt[wv][0] = cand.cnt;
+            s_cnt[wv][1] = cand.conv;
+            s_cnt[wv][2] = cand.ncompact;
+        }
+        __syncthreads();
+        if (wv != 0) return;
+        double ta = 0.0, tb = 0.0, tu = 0.0;
+        for (int v = 0; v < NSPLIT; ++v) {
+            ta += s_part[v][0];
+            tb += s_part[v][1];
+            tu += s_part[v][2];
+        }
+        acc64 = lane == 0 ? ta : 0.0;
+        b64 = lane == 0 ? tb : 0.0;
+        u64 = lane == 0 ? tu : 0.0;
+        to_keys(cand, lane);
+        for (int v = 1; v < NSPLIT; ++v) {
+            const int n = s_cnt[v][0], cv = s_cnt[v][1];
+            cand.ncompact += s_cnt[v][2];
+            const uint64_t* src = s_keys[v];
+            for (int i0 = 0; i0 < n; i0 += WAVE) {
+                if (cand.cnt + WAVE > CAND) {  // cnt > CAND - 64 >= K
+                    compact_topk(cand.keys, cand.scr, cand.cnt, K, lane);
+                    ++cand.ncompact;
+                    cand.cnt = cand.conv = K;
+                }
+                const int i = i0 + lane;
+                if (i < n) {
+                    const uint64_t e = src[i];
+                    cand.keys[cand.cnt + lane] = i < cv ? e : make_key(__uint_as_float((uint32_t)(e >> 32)), (uint32_t)e);
+                }
+                cand.cnt += min(WAVE, n - i0);
+                cand.conv = cand.cnt;
+                lds_fence();
+            }
+        }
+    }
     // speculation check: the buffer holds the true top-K iff at least K elements passed the guess
     // (or a compaction happened, which needs > CAND - TS >= K passes).  Else re-stream, exactly.
     if (spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) {
@@ -1236,8 +1350,26 @@ static int fail(ns_ctx* ctx, int code, const std::string& msg) {
     return code;
 }
 
+// Small batches run the split form (one workgroup of 16 fp32 / 8 fp16 waves per stream) up to this many streams:
+// below it one wave per stream leaves most of the chip idle and the lone wave's dependent chain sets the time.
+static int g_split_max_b = -1;  // < 0: not set yet (environment NSG_SPLIT_MAX_B, else 256: one workgroup per CU)
+
+static int split_max_b() {
+    if (g_split_max_b < 0) {
+        const char* e = getenv("NSG_SPLIT_MAX_B");
+        g_split_max_b = e ? std::max(0, atoi(e)) : 256;
+    }
+    return g_split_max_b;
+}
+
 template <typename T, bool DECODE, int NSK>
 static void launch_one(const nsg::StepParams& p, hipStream_t s) {
+    constexpr int NSPLIT = (64 * NSG_SAMPLE) / (nsg::WAVE * nsg::Elem<T>::W);
+    if (p.spec_j > 0 && !(!DECODE && p.stats) && p.B <= split_max_b()) {
+        hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, false, NSPLIT>), dim3(p.B), dim3(NSPLIT * nsg::WAVE),
+                           0, s, p);
+        return;
+    }
     const dim3 grid((p.B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);
     if (!DECODE && p.stats)  // statistics build (encode / sample only)
         hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, !DECODE>), grid, block, 0, s, p);
@@ -1276,6 +1408,12 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 extern "C" {
 
 const char* ns_version(void) { return "nsgcoder 0.11 gfx950"; }
+
+int ns_set_split_max_batch(int max_batch) {
+    const int prev = split_max_b();
+    g_split_max_b = max_batch < 0 ? 0 : max_batch;
+    return prev;
+}
 
 int ns_max_topk(int logits_dtype) {
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;

@@ -28,6 +28,17 @@ def _torch():
     return torch
 
 
+@pytest.fixture(autouse=True, params=["wave", "split"])
+def coder_form(request):
+    """Every test runs with both single-pass coder forms: one wave per stream, and the small-batch split form
+    (one workgroup per stream, wave 0 merges) forced at every batch size."""
+    from neuralsteganography_amd import _lib
+
+    prev = _lib.set_split_max_batch(0 if request.param == "wave" else 1 << 30)
+    yield request.param
+    _lib.set_split_max_batch(prev)
+
+
 def _ctx(params, B):
     from neuralsteganography_amd.coder import CoderContext
 
