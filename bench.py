@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--optin-window", type=int, default=256,
                     help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-logits (PCIe-inclusive) side figure")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
@@ -181,7 +183,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
-def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0):
+def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None):
     """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
     compute, HIP decode attention) + HIP coder step per token, every stream encoding its full payload from
     the shared 32-token context until the last stream is done (lockstep, like the reference's per-message
@@ -194,7 +196,7 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0):
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
-    B = args.e2e_batch
+    B = batch or args.e2e_batch
     if args.blas:
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
@@ -442,6 +444,8 @@ def main():
     if not args.no_wide:
         out["wide_path"] = wide_path(args, rank, world, dev)
     if not args.no_e2e:
+        if not args.no_c2:  # C2: one message per GPU -- per-token latency of the whole step (small-batch coder form)
+            out["end_to_end_c2"] = end_to_end(args, rank, world, dev, batch=1)
         out["end_to_end"] = end_to_end(args, rank, world, dev)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             out["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
