@@ -97,8 +97,10 @@ const char* ns_version(void);
 int ns_max_topk(int logits_dtype);
 
 /* Single-pass steps of at most `max_batch` streams run the split form (one workgroup of 16 fp32 / 8 fp16 waves per
- * stream) instead of one wave per stream; 0 disables it.  Default 256 (environment NSG_SPLIT_MAX_B).  Process-wide;
- * speed only -- both forms emit the same tokens and bits.  Returns the previous value. */
+ * stream) instead of one wave per stream; 0 disables it, a negative value restores the automatic limit (B * waves
+ * per stream <= 6144: fp32 B <= 384, fp16 B <= 768; environment NSG_SPLIT_MAX_B sets an explicit one).
+ * Process-wide; speed only -- both forms emit the same tokens and bits.  Returns the previous setting (-1:
+ * automatic). */
 int ns_set_split_max_batch(int max_batch);
 
 /* Reset B stream states to [0, 2^precision), bit_pos 0. */

@@ -154,8 +154,9 @@ def version() -> str:
 
 
 def set_split_max_batch(max_batch: int) -> int:
-    """Steps of at most max_batch streams use the split (workgroup-per-stream) coder form; returns the previous
-    limit.  Speed only: both forms give the same tokens and bits."""
+    """Steps of at most max_batch streams use the split (workgroup-per-stream) coder form (negative: the
+    automatic limit); returns the previous setting (-1: automatic).  Speed only: both forms give the same tokens
+    and bits."""
     return int(lib().ns_set_split_max_batch(int(max_batch)))
 
 

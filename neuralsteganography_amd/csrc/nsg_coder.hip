@@ -1350,22 +1350,29 @@ static int fail(ns_ctx* ctx, int code, const std::string& msg) {
     return code;
 }
 
-// Small batches run the split form (one workgroup of 16 fp32 / 8 fp16 waves per stream) up to this many streams:
-// below it one wave per stream leaves most of the chip idle and the lone wave's dependent chain sets the time.
-static int g_split_max_b = -1;  // < 0: not set yet (environment NSG_SPLIT_MAX_B, else 256: one workgroup per CU)
+// Small batches run the split form (one workgroup of 16 fp32 / 8 fp16 waves per stream): below a few thousand
+// streams one wave per stream leaves most of the chip idle and the lone wave's dependent chain sets the time.
+// Automatic limit: B * NSPLIT <= 6144 waves (fp32 B <= 384, fp16 B <= 768; the forms measured equal at 8192,
+// profiles/split_r02y); ns_set_split_max_batch / NSG_SPLIT_MAX_B set an explicit limit for both dtypes.
+static int g_split_max_b = -2;  // -2: not read yet, -1: automatic, >= 0: explicit
 
-static int split_max_b() {
-    if (g_split_max_b < 0) {
+static int split_setting() {
+    if (g_split_max_b == -2) {
         const char* e = getenv("NSG_SPLIT_MAX_B");
-        g_split_max_b = e ? std::max(0, atoi(e)) : 256;
+        g_split_max_b = e ? std::max(0, atoi(e)) : -1;
     }
     return g_split_max_b;
+}
+
+static int split_max_b(int nsplit) {
+    const int v = split_setting();
+    return v >= 0 ? v : 6144 / nsplit;
 }
 
 template <typename T, bool DECODE, int NSK>
 static void launch_one(const nsg::StepParams& p, hipStream_t s) {
     constexpr int NSPLIT = (64 * NSG_SAMPLE) / (nsg::WAVE * nsg::Elem<T>::W);
-    if (p.spec_j > 0 && !(!DECODE && p.stats) && p.B <= split_max_b()) {
+    if (p.spec_j > 0 && !(!DECODE && p.stats) && p.B <= split_max_b(NSPLIT)) {
         hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, false, NSPLIT>), dim3(p.B), dim3(NSPLIT * nsg::WAVE),
                            0, s, p);
         return;
@@ -1407,11 +1414,11 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.11 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.12 gfx950"; }
 
 int ns_set_split_max_batch(int max_batch) {
-    const int prev = split_max_b();
-    g_split_max_b = max_batch < 0 ? 0 : max_batch;
+    const int prev = split_setting();
+    g_split_max_b = max_batch < 0 ? -1 : max_batch;
     return prev;
 }
 
