@@ -47,3 +47,18 @@ def test_no_gpu_means_loud_failure():
 
     with pytest.raises(_lib.NativeLibraryError):
         CoderContext(CoderParams(vocab=50257), max_batch=4)
+
+
+def test_split_form_setting_round_trips():
+    """ns_set_split_max_batch is host-only state: an explicit limit, 0 (off) and a negative value (automatic,
+    reported as -1) round-trip, and the previous setting comes back."""
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("libnsgcoder.so not built (run __graft_entry__.build())")
+    prev = _lib.set_split_max_batch(100)
+    try:
+        assert _lib.set_split_max_batch(0) == 100
+        assert _lib.set_split_max_batch(-5) == 0
+        assert _lib.set_split_max_batch(7) == -1
+        assert _lib.set_split_max_batch(7) == 7
+    finally:
+        _lib.set_split_max_batch(prev)
