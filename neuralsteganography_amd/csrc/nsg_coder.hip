@@ -1372,9 +1372,13 @@ static int split_max_b(int nsplit) {
 template <typename T, bool DECODE, int NSK>
 static void launch_one(const nsg::StepParams& p, hipStream_t s) {
     constexpr int NSPLIT = (64 * NSG_SAMPLE) / (nsg::WAVE * nsg::Elem<T>::W);
-    if (p.spec_j > 0 && !(!DECODE && p.stats) && p.B <= split_max_b(NSPLIT)) {
-        hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, false, NSPLIT>), dim3(p.B), dim3(NSPLIT * nsg::WAVE),
-                           0, s, p);
+    if (p.spec_j > 0 && p.B <= split_max_b(NSPLIT)) {
+        if (!DECODE && p.stats)  // statistics build: the per-wave partials of the extra sums merge like the fast sum
+            hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, !DECODE, NSPLIT>), dim3(p.B),
+                               dim3(NSPLIT * nsg::WAVE), 0, s, p);
+        else
+            hipLaunchKernelGGL((nsg::coder_step_kernel<T, DECODE, NSK, false, NSPLIT>), dim3(p.B),
+                               dim3(NSPLIT * nsg::WAVE), 0, s, p);
         return;
     }
     const dim3 grid((p.B + nsg::WPB - 1) / nsg::WPB), block(nsg::WPB * nsg::WAVE);

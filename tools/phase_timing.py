@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--topk", type=int, default=300)
+    ap.add_argument("--stats", action="store_true", help="statistics build (EncodeSession(stats=True))")
+    ap.add_argument("--full-only", action="store_true", help="time the full step only")
     a = ap.parse_args()
     if a.lib:
         os.environ["NSG_CODER_LIB"] = a.lib
@@ -39,10 +41,12 @@ def main():
         g.manual_seed(i)
         pool.append((3.0 * torch.randn((B, ld), generator=g, device="cuda")).to(params.torch_dtype))
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 1024)) for s in range(B)]
-    sess = EncodeSession(ctx, bits)
+    sess = EncodeSession(ctx, bits, stats=a.stats)
     sess.enable_trace()
     phases = [("stream_no_cand", _lib.NS_STEP_DIAG_NO_CANDIDATES), ("stream_cand", _lib.NS_STEP_DIAG_STREAM_ONLY),
               ("stream_cand_rank", _lib.NS_STEP_DIAG_SKIP_CDF), ("full", 0)]
+    if a.full_only:
+        phases = phases[-1:]
     for name, fl in phases:
         for t in range(3):
             sess.step(pool[t % 4], diag_flags=fl)
