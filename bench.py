@@ -1,22 +1,28 @@
-"""Benchmark of the batched arithmetic-coding hot path (BASELINE.json metric).
+"""Benchmark of the batched arithmetic-coding stego path (BASELINE.json metric).
 
-Workload (config C3, one MI355X): B = 4096 independent streams, 1 KiB random payload each, GPT-2-small
-vocabulary V = 50,257, fp32 logits resident in HBM, temp 0.9, precision 26, topk 300, banned {V-1, 628}.
-A *step* is one coder step (top-k, float64 CDF, interval update, bit consume) over all B streams, i.e. one
-`ns_encode_step` launch over a [B, ld] logit matrix.  Logits come from a pool of distinct synthetic
-batches (3*N(0,1), far larger than the 256 MiB Infinity Cache) cycled step by step; each stream's payload
-cursor advances for real, so every step does new work.
+Headline (config C3, one MI355X per rank): GPT-2-small (random-init weights of that architecture, fp16 compute,
+fp16 logits) + the HIP coder, B = 4096 independent streams per GPU, each encoding a 1 KiB random payload from
+the shared 32-token context to completion (temp 0.9, precision 26, topk 300, banned {V-1, 628}).  A *step* is
+one lockstep token step over all B streams: the coder step on the current logits, then the batch-invariant GPT-2
+decode step that turns its tokens into the next logits (captured once as a hipGraph and replayed).  The whole
+job is timed: ``value`` = payload bits encoded per second over all ranks, ``ms_per_step`` = job time / lockstep
+steps.  The covers are then decoded (timed separately) and ``roundtrip_exact_fraction`` = share of streams whose
+payload came back bit for bit.
 
-value = payload bits fixed per second over the whole job (sum over ranks); cover tokens/s is reported
-beside it.  Multi-GPU: one process per GPU, each with its own B streams (weak scaling, no collective on
-the data path).  Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+``coder``: the coder hot path alone (SURVEY §8(d)'s roofline unit): ``--steps K`` launches of ``ns_encode_step``
+over B resident [B, ld] synthetic 3*N(0,1) logit batches after ``--warmup W``, the K launches captured as one
+hipGraph and replayed; ``roofline`` is that kernel's (HBM-bound).  ``cpu_baseline``: the oracle port on the host
+cores (rank 0, N = 1).
+
+Multi-GPU: one process per GPU, each with its own B streams (weak scaling, no collective on the data path; the
+only collectives are the end-of-job reductions).  Launch: python bench.py [--gpus N --steps K --warmup W]; N>1
+under torch.distributed.run.
 """
 
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -28,13 +34,19 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "payload bits/sec + cover tokens/sec, GPT-2 arithmetic stego at batch, 1-8 GPUs"
 
 
-def parse():
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200, help="coder sub-benchmark: timed launches")
+    ap.add_argument("--warmup", type=int, default=20, help="coder sub-benchmark: untimed launches")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=int, default=50257)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16"])
@@ -42,13 +54,19 @@ def parse():
     ap.add_argument("--topk", type=int, default=300)
     ap.add_argument("--temp", type=float, default=0.9)
     ap.add_argument("--payload-bytes", type=int, default=1024)
-    ap.add_argument("--pool", type=int, default=6, help="distinct logit batches cycled over the steps")
+    ap.add_argument("--pool", type=int, default=6, help="distinct logit batches cycled over the coder steps")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-e2e-seconds", type=float, default=10.0,
                     help="end-to-end CPU baseline (HF GPT-2 forward + oracle coder per core); 0 = skip")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end GPT-2 + coder leg")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip every end-to-end GPT-2 leg (the headline is then the coder sub-benchmark)")
+    ap.add_argument("--no-decode", action="store_true", help="headline: skip the decode / round-trip check")
     ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the gpt2-fa geometry leg (config C4's per-GPU share: 4096 streams, V = 42,001)")
+    ap.add_argument("--c5", action="store_true",
+                    help="add the C5 per-GPU share: GPT-2-medium fp16, topk 100, 1024 streams (coder config only)")
     ap.add_argument("--fp8kv", action="store_true", help="add the fp8-KV-cache end-to-end side line (opt-in mode)")
     ap.add_argument("--optin-window", type=int, default=256,
                     help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
@@ -68,10 +86,10 @@ def parse():
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
                     help="logits handed to the coder; the fp16 head GEMM's output either way (f32 = upcast copy)")
     ap.add_argument("--eager", action="store_true",
-                    help="time eager launches (one event pair each) instead of the replayed hipGraph of the K steps")
+                    help="coder: time eager launches (one event pair each) instead of the replayed hipGraph")
     ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch measured by a rocprofv3 --pmc pass (corrected), if known")
-    return ap.parse_args()
+                    help="HBM bytes per coder launch measured by a rocprofv3 --pmc pass (corrected), if known")
+    return ap.parse_args(argv)
 
 
 def _cpu_workers(module, argv, seconds, max_workers=16):
@@ -134,7 +152,7 @@ def cpu_baseline(args, seconds, streams_per_core=16):
 def wide_path(args, rank, world, dev, steps=10, warmup=3):
     """The api default quality (precision 16, topk 50,000: api.py:81-86) at the coder batch: the wide path
     (csrc/nsg_wide.hip) on resident 3*N(0,1) fp32 logits, 1-KiB payloads, whole steps timed with HIP events on
-    the launch stream.  A side line: the headline is the code_base C3 configuration above."""
+    the launch stream.  A side line."""
     import torch
     import torch.distributed as dist
 
@@ -158,6 +176,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
         sess.step(pool[t % 3])
     bp0 = sess.fields()["bit_pos"].astype("int64").sum()
     nt0 = sess.fields()["ntokens"].astype("int64").sum()
+    c0 = ctx.counters()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -170,6 +189,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
     elapsed = start.elapsed_time(end) / 1e3
     sess.raise_errors()
     f = sess.fields()
+    c1 = ctx.counters()
     nbits = int(f["bit_pos"].astype("int64").sum() - bp0)
     ntok = int(f["ntokens"].astype("int64").sum() - nt0)
     bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
@@ -179,67 +199,114 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
     return {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
             "ms_per_step": 1e3 * el_max / steps, "steps": steps,
             "achieved_gbs": alg / (el_max / steps) / 1e9, "peak_gbs": HBM_PEAK_GBS,
+            "frac": alg / (el_max / steps) / 1e9 / HBM_PEAK_GBS,
+            "listed_stream_step_fraction": (c1[0] - c0[0]) / max(ntok, 1),
             "workload": f"api default quality: {B} streams/GPU x ns_encode_step, precision 16, topk 50000, temp 1.0, "
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
-def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None):
-    """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
-    compute, HIP decode attention) + HIP coder step per token, every stream encoding its full payload from
-    the shared 32-token context until the last stream is done (lockstep, like the reference's per-message
-    loop run for all messages at once).  Wall clock around HipArithmeticLM.encode_batch, max over ranks."""
+def rank_payloads(total, world, rank, nbytes):
+    """This rank's payload bit lists: streams ``shard_range(total, world, rank)`` (contiguous slices), stream s
+    carrying ``synthetic.payload_bytes(s, nbytes)`` as LSB-first bits, so the union over ranks is
+    the same stream set whatever the world size."""
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.dist import shard_range
+
+    return [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in shard_range(total, world, rank)]
+
+
+def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=None):
+    """One timed whole job on this rank: ``lm.encode_batch`` of the rank's streams to completion, bracketed by a
+    barrier and a device synchronisation on both sides; then (``decode``) ``lm.decode_batch`` of the covers,
+    timed the same way, and the share of streams whose payload came back bit for bit.  Totals are summed over
+    ranks and times maxed (``dist.reduce_job``); ``per_rank_*`` expose load imbalance.  Works on
+    any provider with ``encode_batch`` / ``decode_batch`` (the gloo test drives it with a CPU stand-in)."""
     import torch
     import torch.distributed as dist
 
+    from neuralsteganography_amd.dist import per_rank, reduce_job
+
+    def sync():
+        if getattr(dev, "type", "cpu") == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        res = fn()
+        sync()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        return res, dt
+
+    toks, elapsed = timed(lambda: lm.encode_batch(bit_lists, context, quality=quality, graphs=graphs))
+    nbits = sum(len(b) for b in bit_lists)
+    ntok = sum(len(t) for t in toks)
+    steps = max((len(t) for t in toks), default=0)
+    bits_all, tok_all, el_max, steps_max = reduce_job(nbits, ntok, elapsed, float(steps), device=dev)
+    out = {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
+           "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max, "payload_bits": bits_all,
+           "cover_tokens": tok_all, "streams": int(round(reduce_job(len(bit_lists), 0, 0, 0, device=dev)[0])),
+           "per_rank_seconds": per_rank(elapsed, device=dev),
+           "per_rank_lockstep_steps": [int(v) for v in per_rank(steps, device=dev)],
+           "lockstep_steps": int(steps_max), "ms_per_step": 1e3 * el_max / max(steps_max, 1),
+           "bits_per_token": bits_all / max(tok_all, 1)}
+    if decode:
+        dec, dt = timed(lambda: lm.decode_batch(toks, context, quality=quality, graphs=graphs))
+        exact = sum(1 for d, b in zip(dec, bit_lists) if list(d[: len(b)]) == list(b))
+        ex_all, n_all, dt_max, _ = reduce_job(exact, len(bit_lists), dt, 0.0, device=dev)
+        out["roundtrip_exact_fraction"] = ex_all / max(n_all, 1)
+        out["roundtrip_exact_streams"] = int(ex_all)
+        out["decode"] = {"seconds": dt_max, "value": bits_all / dt_max, "unit": "payload bits/s",
+                         "cover_tokens_per_s": tok_all / dt_max, "ms_per_step": 1e3 * dt_max / max(steps_max, 1),
+                         "per_rank_seconds": per_rank(dt, device=dev)}
+    return out
+
+
+def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, model=None, topk=None,
+               decode=False):
+    """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
+    compute, HIP decode step) + HIP coder step per token, every stream encoding its full payload from the shared
+    32-token context until the last stream is done (lockstep, like the reference's per-message loop run for all
+    messages at once); ``decode`` adds the decode and the round-trip check (:func:`e2e_job`)."""
+    import torch
+
     from neuralsteganography_amd import synthetic
-    from neuralsteganography_amd.dist import per_rank, reduce_job, shard_range
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
     B = batch or args.e2e_batch
+    model = model or args.e2e_model
+    topk = topk or args.topk
     if args.blas:
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
-    lm = HipArithmeticLM(random_gpt2(args.e2e_model), None, device=str(dev), logits_dtype=args.e2e_logits,
+    lm = HipArithmeticLM(random_gpt2(model), None, device=str(dev), logits_dtype=args.e2e_logits,
                          max_batch=B, kv_dtype=kv_dtype, attention_window=window)
     lm.lm.position_cap = args.e2e_kv_cap
     lm.lm.chunked_cache = args.e2e_kv_layout == "chunked"
-    quality = {"temp": args.temp, "precision": args.precision, "topk": args.topk}
+    quality = {"temp": args.temp, "precision": args.precision, "topk": topk}
     context = synthetic.DEFAULT_CONTEXT
+    graphs = False if args.e2e_eager else None
     # warm-up: kernels and the coder context at the same batch, short payloads; then the full-size KV cache is
     # allocated and written once (a fresh process's first pass over ~250 GB of new allocations measured up to
     # 12 % slower per step than later ones), and handed back to PyTorch's caching allocator for the timed run
-    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality, graphs=False if args.e2e_eager else None)
-    mine = shard_range(B * world, world, rank)
-    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.e2e_payload_bytes)) for s in mine]
+    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality, graphs=graphs)
+    bits = rank_payloads(B * world, world, rank, args.e2e_payload_bytes)
     lm.lm.prefill(context, B, 2 * max(len(b) for b in bits) + 64)
     lm.lm.k_cache.zero_()
     lm.lm.v_cache.zero_()
     lm.lm.k_cache = lm.lm.v_cache = None
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    toks = lm.encode_batch(bits, context, quality=quality, graphs=False if args.e2e_eager else None)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    nbits = sum(len(b) for b in bits)
-    ntok = sum(len(t) for t in toks)
-    steps = max(len(t) for t in toks)
-    bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
-    rank_s, rank_steps = per_rank(elapsed, device=dev), per_rank(steps, device=dev)
-    out = {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
-           "cover_tokens_per_s_per_gpu": tok_all / el_max / world, "seconds": el_max,
-           "per_rank_seconds": rank_s, "per_rank_lockstep_steps": [int(v) for v in rank_steps],
-           "lockstep_steps": steps, "ms_per_step": 1e3 * el_max / steps, "bits_per_token": bits_all / tok_all,
-           "kv_positions": lm.lm.max_len,
-           "kv_dtype": kv_dtype, "attention_window": window or None,
-           "workload": f"{args.e2e_model} (random-init weights, fp16 compute, {args.e2e_logits} logits, {kv_dtype} KV "
-                       f"cache, batch-invariant native decode step) + ns_encode_step, {B} streams/GPU x "
-                       f"{args.e2e_payload_bytes}-byte payloads encoded to completion from a 32-token context, "
-                       + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")}
+    out = e2e_job(lm, bits, context, quality, dev=dev, world=world, decode=decode, graphs=graphs)
+    out.update({"kv_positions": lm.lm.max_len, "kv_dtype": kv_dtype, "attention_window": window or None,
+                "workload": f"{model} (random-init weights, fp16 compute, {args.e2e_logits} logits, {kv_dtype} KV "
+                            f"cache, batch-invariant native decode step) + ns_encode_step (temp {args.temp}, "
+                            f"precision {args.precision}, topk {topk}), {B} streams/GPU x {args.e2e_payload_bytes}-"
+                            f"byte payloads encoded to completion from a 32-token context, "
+                            + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")})
     del lm
     torch.cuda.empty_cache()
     return out
@@ -287,22 +354,16 @@ def measured_traffic(args, version):
     return best
 
 
-def main():
-    args = parse()
+def coder_bench(args, rank, world, dev):
+    """The coder hot path alone: K launches of ns_encode_step over B resident synthetic logit rows (a pool of
+    distinct batches, far larger than the 256 MiB Infinity Cache, cycled step by step; every stream's payload
+    cursor advances for real).  Returns the sub-object, its ``roofline`` included."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
-
-    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd import _lib, synthetic
     from neuralsteganography_amd.coder import CoderContext, CoderParams, EncodeSession, row_stride
+    from neuralsteganography_amd.dist import per_rank, reduce_job, shard_range
 
     B, V = args.batch, args.vocab
     params = CoderParams(vocab=V, precision=args.precision, temp=args.temp, topk=args.topk, dtype=args.dtype)
@@ -316,8 +377,6 @@ def main():
         x = torch.randn((B, ld), generator=gen, device=dev, dtype=torch.float32).mul_(3.0)
         pool.append(x.to(tdt))
         del x
-    from neuralsteganography_amd.dist import per_rank, reduce_job, shard_range
-
     mine = shard_range(B * world, world, rank)  # weak scaling: B streams per rank, disjoint payload seeds
     payload_bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, args.payload_bytes)) for s in mine]
     sess = EncodeSession(ctx, payload_bits)
@@ -344,8 +403,8 @@ def main():
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     graph = None
     if not args.eager:
-        # headline: the K timed steps captured once as a hipGraph and replayed (as the product's token loop
-        # replays its captured step), so the step time is the launches' own, without host launch gaps
+        # the K timed steps captured once as a hipGraph and replayed (as the product's token loop replays its
+        # captured step), so the step time is the launches' own, without host launch gaps
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for t in range(args.steps):
@@ -380,18 +439,12 @@ def main():
     else:
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     stream_steps = int(f1["ntokens"].sum() - f0["ntokens"].sum())
-    exact_steps = c1[0] - c0[0]
-    overflow_compactions = c1[1] - c0[1]
-    spec_misses = c1[2] - c0[2]
     bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
     sess.raise_errors()
     pcie = None if args.no_pcie else host_logits_rate(args, sess, pool[0], stream)
 
     bits_all, ss_all, elapsed_max, kern_ms_max = reduce_job(bits, stream_steps, elapsed, kern_ms, device=dev)
     rank_s = per_rank(elapsed, device=dev)
-
-    from neuralsteganography_amd import _lib
-
     traffic = measured_traffic(args, _lib.version())
     if args.traffic_bytes is not None:
         traffic = (args.traffic_bytes, "command line")
@@ -399,59 +452,104 @@ def main():
     per_stream_step = V * esz + 76  # logit row + state r/w (64) + token (4) + history (4) + payload window (~4)
     alg_bytes = B * per_stream_step
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-
     out = {
-        "metric": "payload bits/sec + cover tokens/sec, GPT-2 arithmetic stego at batch, 1-8 GPUs",
-        "value": bits_all / elapsed_max,
-        "unit": "payload bits/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed_max / args.steps,
-        "per_rank_seconds": rank_s,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic",
-        "config": {
-            "workload": f"C3 coder hot path: {B} streams/GPU x 1 step of ns_encode_step on resident [{B},{ld}] "
-                        f"{args.dtype} logits (GPT-2-small vocab {V}), temp {args.temp}, precision "
-                        f"{args.precision}, topk {args.topk}, {args.payload_bytes}-byte payloads",
-            "global_batch": B * world, "vocab": V, "logits_dtype": args.dtype, "precision": args.precision,
-            "topk": args.topk, "temp": args.temp, "payload_bytes": args.payload_bytes, "logit_pool": args.pool,
-            "parallelism": f"dp{world} (independent streams, no collective)",
-        },
-        "cover_tokens_per_s": ss_all / elapsed_max,
-        "bits_per_token": bits_all / max(ss_all, 1.0),
+        "value": bits_all / elapsed_max, "unit": "payload bits/s", "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed_max / args.steps, "per_rank_seconds": rank_s,
+        "cover_tokens_per_s": ss_all / elapsed_max, "bits_per_token": bits_all / max(ss_all, 1.0),
         "kernel_ms_avg": kern_ms,
         "timing": ("K launches captured in one hipGraph, replayed once; kernel_ms_avg = replay time / K (HIP "
                    "events on the launch stream)") if not args.eager else "eager launches, one event pair each",
         "eager_launches": eager,  # the first min(K, 50) steps after the warm-up, launched one by one
-        "exact_sum_fraction": exact_steps / max(stream_steps, 1),
-        "overflow_compactions_per_stream_step": overflow_compactions / max(stream_steps, 1),
-        "speculation_miss_fraction": spec_misses / max(stream_steps, 1),
+        "exact_sum_fraction": (c1[0] - c0[0]) / max(stream_steps, 1),
+        "overflow_compactions_per_stream_step": (c1[1] - c0[1]) / max(stream_steps, 1),
+        "speculation_miss_fraction": (c1[2] - c0[2]) / max(stream_steps, 1),
+        "workload": f"C3 coder hot path: {B} streams/GPU x 1 step of ns_encode_step on resident [{B},{ld}] "
+                    f"{args.dtype} 3N(0,1) logits (GPT-2-small vocab {V}), temp {args.temp}, precision "
+                    f"{args.precision}, topk {args.topk}, {args.payload_bytes}-byte payloads",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None,
-                     "kernel": f"coder_step_kernel<{'_Float16' if args.dtype == 'f16' else 'float'},false>", "alg_bytes_per_launch": alg_bytes},
+                     "kernel": f"coder_step_kernel<{'_Float16' if args.dtype == 'f16' else 'float'},false>",
+                     "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_per_stream_step": per_stream_step, "stream_steps_per_launch": B},
     }
     if pcie is not None:
         out["host_logits_pcie"] = pcie
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     del pool, sess, ctx
     torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    log("coder sub-benchmark")
+    coder = coder_bench(args, rank, world, dev)
+    roofline = coder.pop("roofline")
+    side = {}
     if not args.no_wide:
-        out["wide_path"] = wide_path(args, rank, world, dev)
+        log("wide path")
+        side["wide_path"] = wide_path(args, rank, world, dev)
+    head = None
     if not args.no_e2e:
+        # headline: config C3 end to end, encoded then decoded and checked
+        log("C3 end to end (encode + decode)")
+        head = end_to_end(args, rank, world, dev, decode=not args.no_decode)
         if not args.no_c2:  # C2: one message per GPU -- per-token latency of the whole step (small-batch coder form)
-            out["end_to_end_c2"] = end_to_end(args, rank, world, dev, batch=1)
-        out["end_to_end"] = end_to_end(args, rank, world, dev)
+            log("C2 end to end")
+            side["end_to_end_c2"] = end_to_end(args, rank, world, dev, batch=1, decode=True)
+        if not args.no_c4:  # C4's per-GPU share: gpt2-fa geometry (V = 42,001), 4096 streams
+            log("C4 share end to end")
+            side["end_to_end_c4"] = end_to_end(args, rank, world, dev, model="gpt2-fa")
+        if args.c5:  # C5's per-GPU share (coder config; the quality guard runs in tests/test_gpu_northstar.py)
+            log("C5 share end to end")
+            side["end_to_end_c5"] = end_to_end(args, rank, world, dev, model="gpt2-medium", batch=1024, topk=100)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
-            out["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
+            log("fp8 KV end to end")
+            side["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
         if args.optin_window:  # opt-in: fp8 KV + sliding attention window (bounded per-step KV traffic)
-            out["end_to_end_optin"] = end_to_end(args, rank, world, dev, kv_dtype="fp8", window=args.optin_window)
-    if want_cpu:
+            log("opt-in end to end")
+            side["end_to_end_optin"] = end_to_end(args, rank, world, dev, kv_dtype="fp8", window=args.optin_window)
+
+    cfg = {"global_batch": args.batch * world, "vocab": args.vocab, "precision": args.precision, "topk": args.topk,
+           "temp": args.temp, "parallelism": f"dp{world} (independent streams, no collective)"}
+    if head is not None:
+        out = {"metric": METRIC, "value": head["value"], "unit": "payload bits/s", "n_gpus": world,
+               "steps": head["lockstep_steps"], "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+               "per_rank_seconds": head["per_rank_seconds"], "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": dict(cfg, workload="C3 end to end: " + head["workload"], global_batch=args.e2e_batch * world,
+                              model=f"{args.e2e_model} (random-init)", lm_dtype="fp16",
+                              logits_dtype=args.e2e_logits, payload_bytes=args.e2e_payload_bytes),
+               "steps_note": ("steps = lockstep token steps of the timed job (every stream's payload encoded to "
+                              "completion); --steps/--warmup set the coder sub-benchmark"),
+               "cover_tokens_per_s": head["cover_tokens_per_s"],
+               "cover_tokens_per_s_per_gpu": head["cover_tokens_per_s_per_gpu"],
+               "bits_per_token": head["bits_per_token"],
+               "roundtrip_exact_fraction": head.get("roundtrip_exact_fraction"),
+               "roofline": roofline, "end_to_end": head, "coder": coder}
+    else:
+        out = {"metric": METRIC, "value": coder["value"], "unit": "payload bits/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": coder["ms_per_step"],
+               "per_rank_seconds": coder["per_rank_seconds"], "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": dict(cfg, workload=coder["workload"], logits_dtype=args.dtype,
+                              payload_bytes=args.payload_bytes),
+               "cover_tokens_per_s": coder["cover_tokens_per_s"], "roofline": roofline, "coder": coder}
+    out.update(side)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baselines")
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -7,6 +7,9 @@
   (``ns_token_probs``).
 * :class:`MockLM` -- the fixed Zipf distribution of ``:17-37`` (host).
 * :class:`CachedLM` -- the LRU memo of ``:40-60`` (host).
+* :class:`ProviderBatchedLM` -- the batched-LM protocol over ANY ``next_token_probs`` provider (the L2 protocol
+  of ``codec/types.py:41-45``), so the rank kernel serves ``encode_with_lm`` / ``decode_with_lm`` for user
+  providers too (``codec/arithmetic.py:122-231`` takes any provider).
 """
 
 from __future__ import annotations
@@ -126,4 +129,112 @@ class HipTransformersLM:
         return self._probs[0].cpu().numpy().copy()
 
 
-__all__ = ["MockLM", "CachedLM", "HipTransformersLM"]
+# probability 0 (or negative / non-finite) as a log-probability: far enough below every real entry that the
+# kernel's canonical exp gives exactly 0 (exp_canon(d) = 0 for d < -700), so the id leaves the support as the
+# reference's ``probs > 0`` mask drops it (codec/arithmetic.py:366-370); finite, so key ranges stay finite
+ZERO_LOGIT_GAP = 800.0
+
+
+def dist_to_row(dist, vocab: int) -> np.ndarray:
+    """A ProbDist (float64 ndarray by id, or ``{id: p}`` dict, ``codec/arithmetic.py:388-398``) as a float64
+    probability row of ``vocab`` entries (absent ids: 0)."""
+    if isinstance(dist, np.ndarray):
+        row = np.asarray(dist, dtype=np.float64).reshape(-1)
+        if row.size > vocab:
+            raise ConfigurationError(f"distribution over {row.size} ids for a {vocab}-id vocabulary")
+        if row.size < vocab:
+            row = np.concatenate([row, np.zeros(vocab - row.size)])
+        return row
+    if isinstance(dist, dict):
+        row = np.zeros(vocab, dtype=np.float64)
+        for tok, prob in dist.items():
+            t = int(tok)
+            if not 0 <= t < vocab:
+                raise ConfigurationError(f"token id {t} outside the {vocab}-id vocabulary")
+            row[t] = float(prob)
+        return row
+    raise TypeError(f"Unsupported probability distribution type: {type(dist)!r}")
+
+
+def dist_vocab(dist) -> int:
+    """Vocabulary size implied by one ProbDist (ndarray length, or the largest dict id + 1)."""
+    if isinstance(dist, np.ndarray):
+        return int(dist.size)
+    if isinstance(dist, dict):
+        return max((int(t) for t in dist), default=-1) + 1
+    raise TypeError(f"Unsupported probability distribution type: {type(dist)!r}")
+
+
+def probs_to_logits(rows: np.ndarray) -> np.ndarray:
+    """float64 probability rows -> float32 log-probability rows whose softmax (temperature 1, the rank kernel's
+    ``_ModelAdapter`` form) has the same support and the same order: log p, and ``max - ZERO_LOGIT_GAP`` for
+    entries that are not positive and finite.  Rows without positive mass stay all-equal (no capacity)."""
+    rows = np.asarray(rows, dtype=np.float64)
+    pos = np.isfinite(rows) & (rows > 0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lg = np.where(pos, np.log(np.where(pos, rows, 1.0)), -np.inf)
+    top = np.max(lg, axis=1, keepdims=True)
+    top = np.where(np.isfinite(top), top, 0.0)
+    lg = np.where(pos, lg, top - ZERO_LOGIT_GAP)
+    return lg.astype(np.float32)
+
+
+class ProviderBatchedLM:
+    """``prefill(context, B, max_new)`` / ``step(tokens)`` over a ``next_token_probs`` provider: every stream's
+    context grows by its emitted token, each step queries the provider once per stream (on the host -- that is
+    the provider protocol) with the context trimmed to ``context_window`` (``_next_distribution``,
+    ``codec/arithmetic.py:337-347``), and hands the kernel ``[B, ld]`` float32 log-probability rows
+    (:func:`probs_to_logits`).  ``first`` is the distribution of ``context`` if the caller already has it (it
+    also fixes the vocabulary size)."""
+
+    takes_full_context = True  # HipRankLM: pass the context untrimmed (no 1022-token cut, no [0] for empty)
+
+    def __init__(self, provider, context, *, context_window: Optional[int] = None, first=None, device=None):
+        import torch
+        from types import SimpleNamespace
+
+        self.provider = provider
+        self.window = int(context_window) if context_window else None
+        self._first_ctx = tuple(int(t) for t in context)
+        self._first = first if first is not None else provider.next_token_probs(self._trim(self._first_ctx))
+        V = dist_vocab(self._first)
+        if V < 2:
+            raise ConfigurationError("the provider's distribution needs at least two token ids")
+        self.shape = SimpleNamespace(vocab=V, n_positions=0)
+        from ..coder import row_stride
+
+        self.ld = row_stride(V, "f32")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ctxs = []
+
+    def _trim(self, ctx):
+        return tuple(ctx[-self.window:]) if self.window is not None and len(ctx) > self.window else tuple(ctx)
+
+    def _rows(self):
+        import torch
+
+        V = self.shape.vocab
+        out = np.full((len(self.ctxs), self.ld), -np.inf, dtype=np.float64)
+        for b, ctx in enumerate(self.ctxs):
+            if ctx == self._first_ctx and self._first is not None:
+                dist = self._first
+            else:
+                dist = self.provider.next_token_probs(self._trim(ctx))
+            out[b, :V] = dist_to_row(dist, V)
+        lg = np.zeros((len(self.ctxs), self.ld), dtype=np.float32)
+        lg[:, :V] = probs_to_logits(out[:, :V])
+        return torch.from_numpy(lg).to(self.device)
+
+    def prefill(self, context, B: int, max_new: int):
+        del max_new
+        self.ctxs = [tuple(int(t) for t in context)] * int(B)
+        return self._rows()
+
+    def step(self, tokens):
+        toks = tokens.detach().cpu().tolist() if hasattr(tokens, "detach") else list(tokens)
+        self._first = None  # only the prefill's query is shared
+        self.ctxs = [ctx + (int(t),) for ctx, t in zip(self.ctxs, toks)]
+        return self._rows()
+
+
+__all__ = ["MockLM", "CachedLM", "HipTransformersLM", "ProviderBatchedLM", "dist_to_row", "probs_to_logits"]

@@ -263,14 +263,43 @@ def _span_end(bits, counts, toks, finish, sent_end) -> Optional[int]:
     return None
 
 
+def _split_double_newlines(ids: List[int], tok) -> List[int]:
+    """``code_base/arithmetic.py:233-242``: a re-tokenised "\\n\\n" (GPT-2 id 628, which the coder never emits:
+    it is banned) is split back into two "\\n" (id 198) -- applied when the tokenizer has those pieces."""
+    if 628 not in ids:
+        return ids
+    try:
+        if tok.decode([628]) != "\n\n" or tok.decode([198]) != "\n":
+            return ids
+    except Exception:  # noqa: BLE001 - a vocabulary without those ids
+        return ids
+    out: List[int] = []
+    for t in ids:
+        out.extend((198, 198) if t == 628 else (t,))
+    return out
+
+
+def _cover_ids(text: str, seed_text: str, seed_ids: List[int], tok) -> Optional[List[int]]:
+    """The cover's token ids after the seed: the text's ids minus the seed's, or -- when the seed's last token
+    merged with the first cover token on re-tokenisation -- the ids of the text after the decoded seed."""
+    ids = seed_to_ids(text, tok)
+    if ids[: len(seed_ids)] == seed_ids:
+        return ids[len(seed_ids):]
+    seed_str = spans_to_text([], seed_ids, tok)
+    if seed_str and text.startswith(seed_str):
+        return seed_to_ids(text[len(seed_str):], tok) if text[len(seed_str):] else []
+    return None
+
+
 def texts_to_spans(texts: Sequence[str], *, seed_text: str, lm, quality: Optional[Mapping[str, object]] = None
                    ) -> List[List[List[int]]]:
     """Recover the token spans of many cover texts (the inverse of ``spans_to_text``, which the reference leaves
     unimplemented, ``codec/textio.py:58-63``).  The text is re-tokenised, the seed's ids are stripped, and the
-    spans are found one per round: every cover's next span is decoded as one stream of a lockstep batch (the
-    provider's ``decode_counted``), the packet completes at a known token and the span ends there or, with
-    ``finish_sent``, at the following sentence end.  Needs a tokenizer whose ``encode(decode(ids)) == ids``
-    for the cover's tokens (a text re-tokenised differently raises ``DecodeDivergenceError``)."""
+    spans are found one per round: every cover's next span is decoded as one stream of a lockstep batch, the
+    packet completes at a known token and the span ends there or, with ``finish_sent``, at the following
+    sentence end.  A text that re-tokenises differently from the emitted ids (GPT-2 BPE merges, also across
+    span boundaries) is repaired while decoding with the reference's heuristics (``code_base/arithmetic.py:
+    233-242,300-342``, the provider's ``decode_counted_repair``): the spans are the repaired ids."""
     from .codec.errors import DecodeDivergenceError
     from .lm.mock import MockLM
     from .stego import _quality_args
@@ -282,19 +311,25 @@ def texts_to_spans(texts: Sequence[str], *, seed_text: str, lm, quality: Optiona
     sent_end = lm.sentence_end_table() if finish else None
     rest: List[List[int]] = []
     for i, text in enumerate(texts):
-        ids = seed_to_ids(text, tok)
-        if ids[: len(seed_ids)] != seed_ids:
-            raise DecodeDivergenceError(f"cover {i} does not start with the seed text's tokens")
-        rest.append(ids[len(seed_ids):])
+        ids = _cover_ids(text, seed_text, seed_ids, tok)
+        if ids is None:
+            raise DecodeDivergenceError(f"cover {i} does not start with the seed text")
+        rest.append(_split_double_newlines(ids, tok))
     context = list(lm.encode_seed(seed_text))
     spans: List[List[List[int]]] = [[] for _ in texts]
     active = [i for i in range(len(texts)) if rest[i]]
     while active:
         lists = [rest[i] for i in active]
-        if hasattr(lm, "decode_counted"):
-            def settled(bits_l, counts_l):
-                return all(_span_end(b, c, l, finish, sent_end) is not None for b, c, l in zip(bits_l, counts_l, lists))
 
+        def settled(bits_l, counts_l, toks_l=None):
+            toks_l = lists if toks_l is None else toks_l
+            return all(_span_end(b, c, l, finish, sent_end) is not None for b, c, l in zip(bits_l, counts_l, toks_l))
+
+        edits_l = [[] for _ in lists]
+        orig = [list(l) for l in lists]
+        if hasattr(lm, "decode_counted_repair"):
+            bits_l, counts_l, lists, edits_l = lm.decode_counted_repair(lists, context, quality=q, done=settled)
+        elif hasattr(lm, "decode_counted"):
             bits_l, counts_l = lm.decode_counted(lists, context, quality=q, done=settled)
         elif isinstance(lm, MockLM):  # identity coder: 8 bits per token
             bits_l = [lm.decode_arithmetic(l, context, quality=q) for l in lists]
@@ -302,10 +337,14 @@ def texts_to_spans(texts: Sequence[str], *, seed_text: str, lm, quality: Optiona
         else:
             raise NotImplementedError("text_to_spans needs a provider with decode_counted (or the mock)")
         nxt = []
-        for i, l, b, c in zip(active, lists, bits_l, counts_l):
+        for i, l, b, c, ed, o in zip(active, lists, bits_l, counts_l, edits_l, orig):
             end = _span_end(b, c, l, finish, sent_end)
             if end is None:
                 raise DecodeDivergenceError(f"cover {i}: no complete packet in the remaining {len(l)} tokens")
+            # the list as it stood after the last repair inside the span (later "repairs" decoded the next span's
+            # tokens out of context); a repair at the span's end may have split a cross-boundary merge, whose
+            # suffix tokens start the next span
+            l = next((snap for p, snap in reversed(ed) if p <= end), o)
             spans[i].append([int(t) for t in l[: end + 1]])
             rest[i] = l[end + 1:]
             if rest[i]:

@@ -251,15 +251,7 @@ class HipArithmeticLM:
         cache = self.__dict__.setdefault("_stop_tables", {})
         tab = cache.get(stop_text)
         if tab is None:
-            if not stop_text:
-                raise ConfigurationError("stop_text must be non-empty")
-            last = stop_text[-1]
-            host = torch.zeros(self.vocab, dtype=torch.bool)
-            for i in range(self.vocab):
-                try:
-                    host[i] = last in self.tokenizer.decode([i])
-                except Exception:
-                    host[i] = True  # undecodable alone: always check it on the host
+            host = torch.from_numpy(stop_candidates(self.tokenizer, self.vocab, stop_text))
             tab = cache[stop_text] = host.to(self.device)
         return tab
 
@@ -480,25 +472,46 @@ class HipArithmeticLM:
         ranked ids (:300-342, :func:`bpe_repair`), the token list is edited as the reference edits it, and
         the step is re-issued; an unrepairable token decodes as rank 0 while the LM is still fed the
         received token, exactly as the reference does.  Returns every emitted bit per stream."""
+        return self.decode_counted_repair(token_lists, context, quality=quality, enc=enc, strict=True)[0]
+
+    def decode_counted_repair(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                              quality: Mapping[str, object], enc=None, done=None, check_every: int = 64,
+                              strict: bool = False):
+        """:meth:`decode_tokens_repair` that also returns, per stream, the cumulative number of bits emitted
+        after each token of the (repaired) list and the repaired token list itself -- the span splitter of
+        ``texts_to_spans`` needs both when a cover text re-tokenises differently from the emitted ids.
+        ``done(bits_lists, counts_lists, token_lists) -> bool`` is polled every ``check_every`` tokens and ends
+        the loop early once it holds.  With ``strict`` a repaired token that still falls outside the top-k
+        raises :class:`DecodeDivergenceError`; otherwise that stream stops emitting (its counts stay flat).
+        Returns ``(bits per stream, counts per stream, token lists, edits)``: ``edits[b]`` lists ``(p, list)``,
+        the stream's token list after each repair at position ``p`` (a repair at ``p`` changes positions >= p
+        only), so a caller that learns afterwards that the stream ended at token e takes the list of the last
+        repair at p <= e -- tokens decoded past e (another span's, out of context) may have been "repaired"."""
         import torch
+
+        from ..coder import _state_fields
 
         enc = enc if enc is not None else self.tokenizer
         lists = [[int(t) for t in tl] for tl in token_lists]
         B = len(lists)
         if B == 0:
-            return []
+            return [], [], [], []
+        for tl in lists:  # received ids feed the embedding gather: validate on the host first
+            if any(not 0 <= t < self.vocab for t in tl):
+                raise ConfigurationError(f"received token id outside [0, {self.vocab})")
         params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
         ctx = self._coder(params, B)
         sess = StreamingDecodeSession(ctx, B, max_tokens=max(len(x) for x in lists) + 8)
         logits = self.lm.prefill(context, B, max(len(x) for x in lists) + 8)
         pos = [0] * B
+        counts: List[List[int]] = [[] for _ in range(B)]
+        edits: List[list] = [[] for _ in range(B)]
+        dead = [False] * B  # non-strict: a stream whose repaired token still diverged stops here
+        steps = 0
         while True:
-            active = [pos[b] < len(lists[b]) for b in range(B)]
+            active = [pos[b] < len(lists[b]) and not dead[b] for b in range(B)]
             if not any(active):
                 break
-            for b in range(B):
-                if active[b] and not 0 <= lists[b][pos[b]] < self.vocab:
-                    raise ConfigurationError(f"received token id outside [0, {self.vocab})")
             tok = [lists[b][pos[b]] if active[b] else 0 for b in range(B)]
             last = [active[b] and pos[b] == len(lists[b]) - 1 for b in range(B)]
             sess.step(logits, tok, last, active)
@@ -507,25 +520,41 @@ class HipArithmeticLM:
             if bad:
                 redo = [0] * B
                 for b in bad:
-                    ids = sess.ranked_ids(b)
-                    coder_tok, fixed = bpe_repair(enc, lists[b], pos[b], ids)
+                    ranked = sess.ranked_ids(b)
+                    try:
+                        coder_tok, _ = bpe_repair(enc, lists[b], pos[b], ranked)
+                    except IndexError:  # a merge candidate runs past the end of the text: unrepairable
+                        coder_tok = int(ranked[0])
+                    if any(not 0 <= t < self.vocab for t in lists[b]):
+                        raise ConfigurationError(f"repair produced a token id outside [0, {self.vocab})")
                     redo[b] = coder_tok
                     feed[b] = lists[b][pos[b]]  # repaired token, or the received one when unrepairable
+                    edits[b].append((pos[b], list(lists[b])))
                 sess.clear(bad)
                 act2 = [b in bad for b in range(B)]
                 last2 = [act2[b] and pos[b] == len(lists[b]) - 1 for b in range(B)]
                 sess.step(logits, redo, last2, act2)
                 still = sess.diverged()
                 if still:
-                    from ..codec.errors import DecodeDivergenceError
+                    if strict:
+                        from ..codec.errors import DecodeDivergenceError
 
-                    raise DecodeDivergenceError(f"streams {still[:8]}: repaired token still outside the top-k")
+                        raise DecodeDivergenceError(f"streams {still[:8]}: repaired token still outside the top-k")
+                    sess.clear(still)
+                    for b in still:
+                        dead[b] = True
+            bit_pos = _state_fields(sess.state)["bit_pos"]
             for b in range(B):
-                if active[b]:
+                if active[b] and not dead[b]:
+                    counts[b].append(int(bit_pos[b]))
                     pos[b] += 1
-            if any(pos[b] < len(lists[b]) for b in range(B)):
-                logits = self.lm.step(torch.tensor(feed, device=self.device, dtype=torch.long))
-        return sess.bits()
+            steps += 1
+            if not any(pos[b] < len(lists[b]) and not dead[b] for b in range(B)):
+                break
+            if done is not None and steps % check_every == 0 and done(sess.bits(), counts, lists):
+                break
+            logits = self.lm.step(torch.tensor(feed, device=self.device, dtype=torch.long))
+        return sess.bits(), counts, lists, edits
 
     def sample_batch(self, B: int, length: int, context: Sequence[int], *, temperature: float = 1.0,
                      topk: int = -1, seed: int = 0, stream_offset: int = 0, stats: bool = True):
@@ -545,6 +574,43 @@ class HipArithmeticLM:
             if t + 1 < length:
                 logits = self.lm.step(tok.to(torch.long))
         return sess.tokens(), (sess.stats() if stats else None)
+
+
+def stop_candidates(tokenizer, vocab: int, stop_text: str):
+    """Per-id bool table of the tokens that can complete a new occurrence of ``stop_text`` (the newest token of
+    ``stop_text in enc.decode(output)``, ``code_base/arithmetic.py:207-210``): the id's lone text contains the
+    last character of ``stop_text``.  When that character is more than one UTF-8 byte, a byte-level BPE can
+    split it across tokens and the completing token's lone text is U+FFFD (``errors='replace'``) or empty
+    (``errors='ignore'``): such ids -- lone text with U+FFFD, empty, or not re-encoding to the id -- are
+    candidates too, and so is an id whose lone decode raises."""
+    import numpy as np
+
+    if not stop_text:
+        raise ConfigurationError("stop_text must be non-empty")
+    last = stop_text[-1]
+    multibyte = len(last.encode("utf-8")) > 1
+    tab = np.zeros(vocab, dtype=np.bool_)
+    for i in range(vocab):
+        try:
+            txt = tokenizer.decode([i])
+        except Exception:
+            tab[i] = True  # undecodable alone: always check it on the host
+            continue
+        if last in txt:
+            tab[i] = True
+        elif multibyte:
+            if not txt or "\ufffd" in txt:
+                tab[i] = True
+                continue
+            try:
+                try:
+                    back = list(tokenizer.encode(txt, add_special_tokens=False))
+                except TypeError:
+                    back = list(tokenizer.encode(txt))
+            except Exception:
+                back = None
+            tab[i] = back != [i]
+    return tab
 
 
 def bpe_repair(enc, inp: List[int], i: int, ranked_ids: Sequence[int]):
@@ -584,4 +650,4 @@ def bpe_repair(enc, inp: List[int], i: int, ranked_ids: Sequence[int]):
     return int(ranked_ids[0]), False
 
 
-__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality", "bpe_repair"]
+__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality", "bpe_repair", "stop_candidates"]

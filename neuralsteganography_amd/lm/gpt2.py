@@ -142,6 +142,7 @@ class BatchedGPT2:
             return int(want)
         free, _ = torch.cuda.mem_get_info(self.device)
         # memory PyTorch's caching allocator holds but no tensor uses (e.g. a previous call's KV cache) is free too
+        # (the allocator releases cached blocks and retries when a request does not fit one of them)
         free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         if self.k_cache is not None:
             free += 2 * self.k_cache.numel() * self.k_cache.element_size()
@@ -283,6 +284,8 @@ class BatchedGPT2:
             kp, vp = self.k_cache, self.v_cache  # [n_layer, 1, H, T, D]
             if self.kv_dtype == "fp8":  # the context rows get the same conversion as the decode-time appends
                 kp, vp = self._quantize_fp8(kp), self._quantize_fp8(vp)
+            # the one-stream prefill cache survives as kp/vp: it is not free memory for the stream cache
+            self.k_cache = self.v_cache = None
             self.allocate(B, T + self.fit_positions(B, max_new), T0=T)
             self.kp, self.vp = kp, vp
         else:

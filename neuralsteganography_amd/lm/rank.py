@@ -124,11 +124,29 @@ class HipRankLM:
         self._decode_states = deque(dict(s) for s in states)
 
     # ------------------------------------------------------------------ batched
+    def _context(self, context: Sequence[int]) -> List[int]:
+        """The prefill context: GPT-2 keeps the reference's last 1022 ids (and needs one); a host provider
+        (``ProviderBatchedLM``) gets it untrimmed, as ``next_token_probs`` would."""
+        if getattr(self.lm, "takes_full_context", False):
+            return [int(t) for t in context]
+        return list(context)[-1022:] or [0]
+
     def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], max_steps: int = 1 << 16) -> List[List[int]]:
+        toks, states = self.encode_batch_states(bit_lists, context, quality=quality, max_steps=max_steps)
+        for st in states:
+            self._encode_states.append(dict(st))
+            self._decode_states.append(dict(st))
+        return toks
+
+    def encode_batch_states(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
+                            quality: Mapping[str, object], max_steps: int = 1 << 16):
+        """:meth:`encode_batch` returning ``(tokens, states)`` -- each stream's ``{"history", "residual_bits"}``
+        side channel -- without queueing the states on the provider (``codec.rank.encode_with_lm`` hands them
+        to the caller's ``state`` dict instead)."""
         B = len(bit_lists)
         if B == 0:
-            return []
+            return [], []
         payloads = [_bits_to_bytes(list(b)) for b in bit_lists]
         empty = [len(p) == 0 for p in payloads]
         ctx = self._coder(B)
@@ -138,22 +156,22 @@ class HipRankLM:
             sess.nbits[[i for i, e in enumerate(empty) if e]] = 0
         import torch
 
-        logits = self.lm.prefill(list(context)[-1022:] or [0], B, 8 * max(len(p) for p in payloads) + 2)
+        logits = self.lm.prefill(self._context(context), B, 8 * max(len(p) for p in payloads) + 2)
+        every = 1 if getattr(self.lm, "takes_full_context", False) else 8  # host providers: no wasted queries
         for t in range(max_steps):
-            if t % 8 == 0:
+            if t % every == 0:
                 sess.raise_errors()
                 if sess.all_done():
                     break
             tok = sess.step(logits)
             logits = self.lm.step(tok.to(torch.long))
         toks, cons = sess.tokens(), sess.consumed()
+        states = []
         for i in range(B):
             if empty[i]:
                 toks[i], cons[i] = [], []
-            st = {"history": tuple(cons[i]), "residual_bits": (8 * len(payloads[i])).to_bytes(8, "big")}
-            self._encode_states.append(dict(st))
-            self._decode_states.append(dict(st))
-        return toks
+            states.append({"history": tuple(cons[i]), "residual_bits": (8 * len(payloads[i])).to_bytes(8, "big")})
+        return toks, states
 
     def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], states: Optional[Sequence[CodecState]] = None) -> List[List[int]]:
@@ -172,7 +190,7 @@ class HipRankLM:
                 raise DecodeDivergenceError(f"token id outside [0, {self.vocab})")
         ctx = self._coder(B)
         sess = RankDecodeSession(ctx, token_lists, hist, temp=_temperature(quality), quality=quality)
-        logits = self.lm.prefill(list(context)[-1022:] or [0], B, max(sess.T, 1) + 1)
+        logits = self.lm.prefill(self._context(context), B, max(sess.T, 1) + 1)
         for t in range(sess.T):
             sess.step(logits)
             if t + 1 < sess.T:

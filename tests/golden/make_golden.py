@@ -276,6 +276,53 @@ def run_rank_config(name, cfg):
     return out
 
 
+# src rank coder over GENERIC next_token_probs providers (codec/arithmetic.py:122-231 with the provider
+# called directly, _next_distribution :337-347): the Zipf MockLM of codec/distribution.py:17-37 (imported from
+# the reference itself) and a context-dependent dict provider (tests/golden/providers.py) with a context window.
+PROVIDER_CONFIGS = {
+    "z1_mock_v32_a12": dict(provider="mock", vocab=32, alpha=1.2, quality=None, nbytes=[16, 3]),
+    "z2_mock_v1000_a11_k300_p09": dict(provider="mock", vocab=1000, alpha=1.1, quality={"top_k": 300, "top_p": 0.9},
+                                       nbytes=[20]),
+    "z3_ctxdict_v500_minp_w6": dict(provider="ctxdict", vocab=500, quality={"min_prob": 1e-3}, max_context=6,
+                                    nbytes=[12, 5]),
+}
+
+
+def make_provider(cfg):
+    if cfg["provider"] == "mock":
+        sys.path.insert(0, str(REF / "src"))
+        from neuralstego.codec.distribution import MockLM  # src/neuralstego/codec/distribution.py:17-37
+
+        return MockLM(vocab_size=cfg["vocab"], alpha=cfg["alpha"])
+    from tests.golden.providers import ContextDictLM
+
+    return ContextDictLM(cfg["vocab"])
+
+
+def run_provider_config(name, cfg):
+    sys.path.insert(0, str(REF / "src"))
+    from neuralstego.codec import arithmetic as src_coder  # src/neuralstego/codec/arithmetic.py
+
+    assert Path(src_coder.__file__).resolve() == (REF / "src/neuralstego/codec/arithmetic.py").resolve()
+    out = {"tokens": [], "tok_off": [0], "cons": [], "payload": [], "pay_off": [0], "decoded": [], "dec_off": [0]}
+    for s, nbytes in enumerate(cfg["nbytes"]):
+        payload = synthetic.payload_bytes(s, nbytes)
+        state = {}
+        toks = src_coder.encode_with_lm(payload, make_provider(cfg), context=synthetic.DEFAULT_CONTEXT,
+                                        quality=cfg["quality"], state=state, max_context=cfg.get("max_context"))
+        dstate = dict(state)
+        dec = src_coder.decode_with_lm(toks, make_provider(cfg), context=synthetic.DEFAULT_CONTEXT,
+                                       quality=cfg["quality"], state=dstate, max_context=cfg.get("max_context"))
+        assert dec == payload, f"{name} stream {s}: reference round trip failed"
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["cons"] += list(state["history"])
+        out["payload"] += list(payload); out["pay_off"].append(len(out["payload"]))
+        out["decoded"] += list(dec); out["dec_off"].append(len(out["decoded"]))
+        print(f"  {name} s={s} bytes={nbytes} tokens={len(toks)} bits/token={8 * nbytes / max(1, len(toks)):.2f}",
+              flush=True)
+    return out
+
+
 # crypto quality LM (src/neuralstego/crypto/arithmetic.py encode_arithmetic / decode_arithmetic over
 # _QualityControlledLM + crypto/quality.py apply_quality): name -> vocab, logit scale, crypto quality
 # (temperature on probabilities, top_k, top_p), payload bytes per stream.  Base provider: the untempered
@@ -364,6 +411,22 @@ def main(names=None):
                     quality=crypto_rank_quality(cfg["quality"]), logit_seed=LOGIT_SEED,
                     payload_seed=synthetic.PAYLOAD_SEED, context=synthetic.DEFAULT_CONTEXT,
                     reference="src/neuralstego/crypto/arithmetic.py encode_arithmetic / decode_arithmetic")
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            consumed=np.asarray(res["cons"], dtype=np.int32),
+            payload=np.asarray(res["payload"], dtype=np.uint8), pay_off=np.asarray(res["pay_off"], np.int64),
+            decoded=np.asarray(res["decoded"], dtype=np.uint8), dec_off=np.asarray(res["dec_off"], np.int64))
+    for name, cfg in PROVIDER_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_provider_config(name, cfg)
+        meta = dict(cfg, name=name, kind="provider", payload_seed=synthetic.PAYLOAD_SEED,
+                    context=synthetic.DEFAULT_CONTEXT,
+                    reference="src/neuralstego/codec/arithmetic.py encode_with_lm / decode_with_lm over "
+                              + ("codec/distribution.py MockLM" if cfg["provider"] == "mock"
+                                 else "tests/golden/providers.py ContextDictLM"))
         np.savez_compressed(
             HERE / f"{name}.npz",
             meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),

@@ -160,3 +160,42 @@ def test_cover_text_round_trip_gpu_provider(finish_sent):
                                  chunk_bytes=24)
     assert all(t.startswith(seed) for t in texts)
     assert cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm) == secrets
+
+
+def test_cover_text_reveal_with_bpe_repair():
+    """Cover TEXT whose re-tokenisation differs from the emitted ids (a greedy longest-match toy tokenizer
+    merges adjacent pieces, also across span boundaries): texts_to_spans repairs the received ids while
+    decoding (code_base/arithmetic.py:300-342 via decode_counted_repair) and the secrets come back.  Covers that
+    re-tokenise exactly must all reveal; covers that do not must reveal too wherever the reference's heuristic
+    repairs every merge (the test requires most of them, and at least one)."""
+    from neuralsteganography_amd.codec.textio import seed_to_ids, spans_to_text
+    from neuralsteganography_amd.cover import cover_reveal_batch
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from neuralsteganography_amd.stego import stego_encode_batch
+    from tests.golden.toy_tokenizer import ToyTokenizer
+
+    V = 700
+    tok = ToyTokenizer(V)
+    m = random_gpt2("tiny", vocab_size=V, n_positions=1024, seed=29)
+    lm = HipArithmeticLM(m, tok, compute_dtype=torch.float32)
+    q = {"temp": 1.0, "precision": 26, "topk": 300, "finish_sent": False}
+    secrets = [synthetic.payload_bytes(s, 5 + 7 * s) for s in range(12)]
+    seed = "abc"
+    res = stego_encode_batch(secrets, chunk_bytes=24, ecc="none", quality=q, seed_text=seed, lm=lm)
+    seed_ids = seed_to_ids(seed, tok)
+    texts, differs = [], []
+    for r in res:
+        text = spans_to_text([list(s) for s in r], seed_ids, tok)
+        texts.append(text)
+        emitted = seed_ids + [t for s in r for t in s]
+        differs.append(tok.encode(text) != emitted)
+    assert any(differs), "no cover re-tokenises differently: pick another seed"
+    got = cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm, return_errors=True)
+    for i, (g, d) in enumerate(zip(got, differs)):
+        if not d:
+            assert g == secrets[i], f"cover {i} re-tokenises exactly but did not reveal"
+    repaired = [i for i, d in enumerate(differs) if d and got[i] == secrets[i]]
+    n_diff = sum(differs)
+    print(f"BPE reveal: {n_diff} of {len(texts)} covers re-tokenise differently, {len(repaired)} revealed")
+    assert repaired and len(repaired) * 2 >= n_diff

@@ -1,0 +1,169 @@
+"""GPU: round trips at the north-star configurations (BASELINE.json ``configs``).
+
+The north star asks for 100 % bit-exact payload recovery at batch 4096 with emitted tokens bit-exact against
+the CPU reference on identical logits.  These tests run the product path (batched GPT-2 decode step on the HIP
+kernels, hipGraph-replayed token loop, HIP coder) at the stated sizes:
+
+* C3: GPT-2-small (random-init, fp16 compute and logits), B = 4096 streams x 1 KiB payloads, encode -> decode,
+  every stream's payload recovered bit for bit; a sample of streams is re-run alone on the eager loop with every
+  step's logits captured, which must give the same tokens (the decode step is batch-invariant) and which the
+  CPU oracle (``oracle/nsg_oracle.c``, pinned by the reference's own outputs) replays token for token.
+* C2: GPT-2-small, B = 1, 1 KiB: every step's logits captured, oracle replay of the whole stream, graph-replayed
+  loop equal to the eager loop, decode round trip.
+* C5-like: GPT-2-medium fp16, topk 100, temp 0.9, finish_sent, quality guard ON (the api's default guard, the
+  regeneration schedule of ``api.py:496-523``) over 1024 secrets in one ``cover_generate_batch``; every secret
+  either passes and is revealed from its cover TEXT, or is rejected after the whole schedule.  Payloads are
+  short (the guard's unigram perplexity grows with the cover length), not C5's coder parameters.
+"""
+
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from neuralsteganography_amd import synthetic
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+Q_C3 = {"temp": 0.9, "precision": 26, "topk": 300}  # run_single.py:21-24
+
+
+def _record_eager(lm, bit_lists, context, quality):
+    """encode_batch on the eager loop with every step's logits copied to the host (fp32 view of the f16 rows)."""
+    seen = []
+    orig_step, orig_prefill = lm.lm.step, lm.lm.prefill
+
+    def rec_prefill(*a, **k):
+        out = orig_prefill(*a, **k)
+        seen.append(out[:, : lm.vocab].float().cpu().numpy())
+        return out
+
+    def rec_step(tok):
+        out = orig_step(tok)
+        seen.append(out[:, : lm.vocab].float().cpu().numpy())
+        return out
+
+    lm.lm.prefill, lm.lm.step = rec_prefill, rec_step
+    try:
+        toks = lm.encode_batch(bit_lists, context, quality=quality, graphs=False)
+    finally:
+        lm.lm.prefill, lm.lm.step = orig_prefill, orig_step
+    return toks, seen
+
+
+def _oracle_replay(seen, s, bits, V, quality):
+    o, _ = oracle.encode_stream(lambda t: seen[t][s], bits, banned=[V - 1, 628], temp=quality["temp"],
+                                precision=quality["precision"], topk=quality["topk"])
+    return o
+
+
+def _free_cache(lm):
+    lm.lm.k_cache = lm.lm.v_cache = None
+    lm.lm.kp = lm.lm.vp = None
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(900)
+def test_c3_gpt2_small_b4096_1kib_roundtrip_bit_exact():
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    B, nbytes = 4096, 1024
+    m = random_gpt2("gpt2", seed=1234)
+    lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=B)
+    ctx = synthetic.DEFAULT_CONTEXT
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in range(B)]
+    t0 = time.perf_counter()
+    toks = lm.encode_batch(bits, ctx, quality=Q_C3)
+    t1 = time.perf_counter()
+    print(f"C3 encode done: {t1 - t0:.1f} s", flush=True)
+    _free_cache(lm)
+    out = lm.decode_batch(toks, ctx, quality=Q_C3)
+    t2 = time.perf_counter()
+    bad = [s for s in range(B) if out[s][: len(bits[s])] != bits[s]]
+    assert not bad, f"{len(bad)} of {B} streams did not round-trip (first: {bad[:8]})"
+    ntok = sum(map(len, toks))
+    print(f"C3 round trip: {B} x {nbytes} B, {ntok} tokens, encode {t1 - t0:.1f} s, decode {t2 - t1:.1f} s")
+    _free_cache(lm)
+    # oracle replay: a sample of streams alone, eager, logits captured (batch-invariant step => same logits)
+    sample = [0, 1777, B - 1]
+    sub, seen = _record_eager(lm, [bits[s] for s in sample], ctx, Q_C3)
+    for j, s in enumerate(sample):
+        assert sub[j] == toks[s], f"stream {s}: alone (eager) != inside the B={B} graph-replayed batch"
+        assert _oracle_replay(seen, j, bits[s], lm.vocab, Q_C3) == toks[s], f"stream {s}: HIP coder != oracle"
+
+
+@pytest.mark.timeout(600)
+def test_c2_gpt2_small_b1_1kib_oracle_replay_every_step():
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    m = random_gpt2("gpt2", seed=1234)
+    lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=1)
+    ctx = synthetic.DEFAULT_CONTEXT
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(7, 1024))]
+    toks_e, seen = _record_eager(lm, bits, ctx, Q_C3)
+    assert len(seen) >= len(toks_e[0])  # prefill + one logits row per later token (+ steps up to the done check)
+    assert _oracle_replay(seen, 0, bits[0], lm.vocab, Q_C3) == toks_e[0]
+    toks_g = lm.encode_batch(bits, ctx, quality=Q_C3)  # the hipGraph-replayed product loop
+    assert toks_g == toks_e
+    for graphs in (True, False):
+        out = lm.decode_batch(toks_g, ctx, quality=Q_C3, graphs=graphs)
+        assert out[0][: len(bits[0])] == bits[0]
+
+
+class _IdTokenizer:
+    """id i <-> " w<i>." (every id ends a sentence but 3), last id = <|endoftext|>: decode/encode round-trip
+    every id, so covers are revealed from their text."""
+
+    def __init__(self, vocab):
+        self.eos_id = vocab - 1
+
+    def _piece(self, i):
+        return "<|endoftext|>" if i == self.eos_id else f" w{i}" + ("." if i != 3 else "")
+
+    def decode(self, ids, skip_special_tokens=False):
+        return "".join("" if (skip_special_tokens and int(i) == self.eos_id) else self._piece(int(i)) for i in ids)
+
+    def encode(self, text, add_special_tokens=False):
+        import re
+
+        return [self.eos_id if mm.group(1) is None else int(mm.group(1))
+                for mm in re.finditer(r"<\|endoftext\|>|w(\d+)", text)]
+
+
+@pytest.mark.timeout(900)
+def test_c5_like_gpt2_medium_topk100_guard_on_1024_secrets():
+    from neuralsteganography_amd.cover import (_ensure_guard, cover_generate_batch, cover_reveal_batch,
+                                               prepare_gate_thresholds)
+    from neuralsteganography_amd.exceptions import QualityGateError
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    n = 1024
+    m = random_gpt2("gpt2-medium", seed=77)
+    lm = HipArithmeticLM(m, _IdTokenizer(50257), logits_dtype="f16", max_batch=2 * n)
+    q = {"temp": 0.9, "precision": 26, "topk": 100, "finish_sent": True}
+    # secrets of 0..255 bytes (one packet each); the gate's perplexity threshold is the median of an ungated
+    # first pass over the same secrets, so roughly half the covers pass at attempt 1 and the regeneration
+    # schedule (seed pool, top_k 80 / 70, temp 0.8 / 0.7) runs for the rest
+    secrets = [synthetic.payload_bytes(s, s % 256) for s in range(n)]
+    seed = "w11. w12. w13"
+    first = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=False)
+    guard = _ensure_guard(None)
+    ppl = sorted(v.metrics["ppl"] for v in guard.evaluate_batch(first, prepare_gate_thresholds(None)))
+    gate = {"max_ppl": float(ppl[n // 2])}
+    out = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=True,
+                               gate_thresholds=gate, regen_attempts=2, return_errors=True)
+    passed = [i for i, t in enumerate(out) if isinstance(t, str)]
+    failed = [i for i, t in enumerate(out) if isinstance(t, QualityGateError)]
+    assert len(passed) + len(failed) == n
+    assert passed and failed, (len(passed), len(failed), gate)
+    for i in failed:
+        assert out[i].reasons  # rejected by the last attempt of the schedule, with its reasons
+    got = cover_reveal_batch([out[i] for i in passed], seed_text=seed, quality=q, ecc="rs", lm=lm)
+    wrong = [i for i, g in zip(passed, got) if g != secrets[i]]
+    assert not wrong, f"{len(wrong)} of {len(passed)} passed covers did not reveal (first: {wrong[:8]})"
+    print(f"C5-like: {n} secrets, gate {gate}, {len(passed)} passed the guard and revealed, {len(failed)} rejected")

@@ -161,3 +161,37 @@ def test_crypto_quality_controlled_probs_match_reference_formula(quality):
     want /= want.sum()
     assert np.abs(got - want).max() < 1e-12
     assert (got > 0).sum() == keep.sum()
+
+
+@pytest.mark.parametrize("name", golden.provider_names())
+def test_encode_with_lm_over_generic_provider_matches_reference(name):
+    """encode_with_lm / decode_with_lm accept ANY next_token_probs provider (the reference's
+    Zipf MockLM, a context-dependent dict provider with max_context): the ProbDists are staged to the device and
+    ranked by the HIP rank kernel; tokens, history and payload equal the reference run's."""
+    from neuralsteganography_amd.codec.rank import decode_with_lm, encode_with_lm
+
+    g = golden.load_rank(name)
+    m = g.meta
+    for s in g.streams:
+        state = {}
+        toks = encode_with_lm(s.payload, golden.make_provider(m), context=m["context"], quality=m["quality"],
+                              state=state, max_context=m.get("max_context"))
+        assert toks == s.tokens, f"{name} stream {s.stream}: tokens differ from the reference"
+        assert list(state["history"]) == s.consumed
+        assert int.from_bytes(state["residual_bits"], "big") == 8 * len(s.payload)
+        dec = decode_with_lm(toks, golden.make_provider(m), context=m["context"], quality=m["quality"],
+                             state=dict(state), max_context=m.get("max_context"))
+        assert dec == s.payload
+
+
+def test_encode_with_lm_generic_provider_queries_the_reference_contexts():
+    """The provider sees exactly the contexts the reference's _next_distribution passes (codec/arithmetic.py:
+    337-347): the seed context, then one more emitted token per step, trimmed to max_context."""
+    from neuralsteganography_amd.codec.rank import encode_with_lm
+    from tests.golden.providers import ContextDictLM
+
+    prov = ContextDictLM(500)
+    ctx = [7, 8, 9, 10, 11, 12, 13, 14]
+    toks = encode_with_lm(b"\x5a\xa5\x0f", prov, context=ctx, quality={"min_prob": 1e-3}, max_context=5)
+    want = [tuple((ctx + toks[:t])[-5:]) for t in range(len(toks))]
+    assert prov.calls[: len(want)] == want

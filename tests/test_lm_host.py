@@ -73,3 +73,35 @@ def test_prefill_rejects_out_of_vocab_ids_on_host():
         g.prefill([1, 2, 700], 2, 4)
     with pytest.raises(ValueError):
         g.prefill([-1, 2], 2, 4)
+
+
+def test_stop_candidates_multibyte_last_character_split_across_tokens():
+    """a stop text whose last character is several UTF-8 bytes can be completed by a token
+    that decodes alone to '' (ByteTokenizer, errors='ignore') or U+FFFD (HF GPT-2, errors='replace'); such ids
+    must be in the per-id stop table, or the stop is never detected.  ASCII last characters keep the plain
+    containment rule."""
+    import numpy as np
+
+    from neuralsteganography_amd.lm.arithmetic import stop_candidates
+
+    tok = ByteTokenizer(300)
+    e_bytes = list("é".encode("utf-8"))  # [0xc3, 0xa9]: the completing token 0xa9 decodes alone to ''
+    tab = stop_candidates(tok, 300, "café")
+    assert tab[e_bytes[1]] and tab[e_bytes[0]]
+    assert not tab[ord("a")] and not tab[ord("x")]
+    # the stop really is in the decoded output once the second byte arrives, and only then
+    out = [ord(c) for c in "caf"] + e_bytes
+    assert "café" not in tok.decode(out[:-1]) and "café" in tok.decode(out)
+
+    class ReplaceTok:  # HF-style byte-level decode with errors='replace'
+        def decode(self, ids):
+            return bytes(int(i) % 256 for i in ids).decode("utf-8", errors="replace")
+
+        def encode(self, text, add_special_tokens=False):
+            return list(text.encode("utf-8"))
+
+    tab2 = stop_candidates(ReplaceTok(), 256, "é")
+    assert tab2[0xa9] and tab2[0xc3] and not tab2[ord("e")]
+    ascii_tab = stop_candidates(tok, 300, "<eos>")
+    assert ascii_tab[ord(">")] and not ascii_tab[0xa9]
+    assert int(np.count_nonzero(ascii_tab)) == 1  # only '>' (ids 256..299 decode to bytes 0..43)

@@ -179,3 +179,29 @@ def test_crypto_quality_extraction_and_validation():
     for bad in [(None, None, 0.0), (0, None, 1.0), (None, 1.5, 1.0), (None, 0.0, 1.0)]:
         with pytest.raises(QualityConfigError):
             _rank_quality(*bad)
+
+
+@pytest.mark.parametrize("name", golden.provider_names())
+def test_oracle_rank_coder_over_generic_providers_matches_reference(name):
+    """encode_with_lm / decode_with_lm over a generic next_token_probs provider (codec/arithmetic.py:122-231):
+    the provider's ProbDist (ndarray or dict) staged as log-probability rows (codec.distribution.probs_to_logits,
+    the rows the GPU path hands the rank kernel) and ranked by the oracle give the reference's tokens and
+    consumption history for the Zipf MockLM and a context-dependent dict provider with a context window."""
+    from neuralsteganography_amd.codec.distribution import dist_to_row, probs_to_logits
+
+    g = golden.load_rank(name)
+    m = g.meta
+    win = m.get("max_context")
+    prov = golden.make_provider(m)
+    V = m["vocab"]
+    for s in g.streams:
+        def row(t, toks=s.tokens):
+            ctx = list(m["context"]) + list(toks[:t])
+            if win and len(ctx) > win:
+                ctx = ctx[-win:]
+            return probs_to_logits(dist_to_row(prov.next_token_probs(tuple(ctx)), V)[None])[0]
+
+        toks, cons = oracle.rank_encode_stream(row, s.payload, temp=1.0, quality=m["quality"])
+        assert toks == s.tokens and cons == s.consumed, f"{name} stream {s.stream}"
+        dec = oracle.rank_decode_stream(row, toks, cons, 8 * len(s.payload), temp=1.0, quality=m["quality"])
+        assert dec == s.payload == s.decoded
