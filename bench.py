@@ -288,7 +288,8 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     lm.lm.position_cap = args.e2e_kv_cap
     lm.lm.chunked_cache = args.e2e_kv_layout == "chunked"
     quality = {"temp": args.temp, "precision": args.precision, "topk": topk}
-    context = synthetic.DEFAULT_CONTEXT
+    # [<|endoftext|>] + 31 ids; the end-of-text id is the vocabulary's last (gpt2-fa: 42,000)
+    context = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     graphs = False if args.e2e_eager else None
     # warm-up: kernels and the coder context at the same batch, short payloads; then the full-size KV cache is
     # allocated and written once (a fresh process's first pass over ~250 GB of new allocations measured up to

@@ -422,4 +422,38 @@ __device__ __forceinline__ bool fast_sum_interval(double S_r, float r, double m,
     return true;
 }
 
+// The same interval with a data-dependent argument term (round 3, the one-pass wide kernel).  The terms are
+// e_i = 2^t_i with t_i = fl(x_i * c32 - fl(r * c32)) (one fma).  Against the exact t*_i = (x_i - r) * log2(e)/T:
+// t_i = t*_i (1 + d_c) (1 + d_f) + D, where d_c is c32's rounding (<= u), d_f the fma's (<= u) and
+// D = r*c32 - fl(r*c32) the rounding of the reference's product -- the SAME for every term, and exactly known
+// (computed in double), so the sum is corrected by 2^-D.  What remains is a relative error of
+// ln2 * 2u * |t_i| per term: summed with the terms as weights, 2u ln2 * A_r / S_r with A_r = sum e_i |t_i|.
+// The kernel accumulates the signed B_t = sum e_i t_i (packed fmas; no abs in packed form), and
+// A_r = -B_t + 2 sum_{t_i >= 0} e_i t_i <= -B_t + 2 max(t_m, 0) S_r  (t_m = the largest argument).
+// A_r / S_r is the e-weighted mean |argument|, a few units for real rows, where the worst-case form above charges
+// every term with 60 + |t_m|: about ten times narrower, so far fewer steps need the exact row sum.  Terms below
+// 2^-200 of the largest add less than V * 2^-200 relative (the constant term).
+__device__ __forceinline__ bool fast_sum_interval_dd(double S_r, double B_t, float r, double m, float c32,
+                                                     double inv_temp, int fp32_terms, double& Sf, double& S_lo,
+                                                     double& S_hi) {
+    const double t_m = (m - (double)r) * (double)c32;
+    if (!(S_r > 0.0 && S_r < 1.0e300) || !(B_t > -1.0e300 && B_t < 1.0e300) || !(t_m <= 100.0 && t_m >= -60.0))
+        return false;
+    const double rc = (double)r * (double)c32;                 // exact (float x float fits a double)
+    const double D = rc - (double)(float)rc;                   // exact: the reference product's rounding
+    const double S_c = S_r * exp_canon(-D * 0.6931471805599453);  // 2^-D
+    const double A = fmax(0.0, -B_t) + 2.0 * fmax(t_m + 1.0e-6, 0.0) * S_r;
+    const double f = exp_canon(((double)r - m) * inv_temp);
+    Sf = S_c * f;
+    const double u24 = 5.9604644775390625e-08;  // 2^-24
+    const double eb = 9.5367431640625e-07                                // v_exp_f32 error (2^-20, generous)
+                      + 2.0 * u24 * 0.6931471805599453 * 1.01 * (A / S_r)  // argument rounding, e-weighted
+                      + (double)(fp32_terms + 1) * u24                     // fp32 partials
+                      + 1.0e-13;
+    const double B2 = 2.0 * eb + 1.0e-12;
+    S_lo = Sf * (1.0 - B2);
+    S_hi = Sf * (1.0 + B2);
+    return true;
+}
+
 }  // namespace nsg

@@ -231,7 +231,8 @@ __global__ void wide_offsets_kernel(int B, int cap, const WideStat* ws, const un
     if (b < B) {
         const unsigned int n = ws[b].active ? count[b] : 0u;
         begin[b] = (unsigned int)(b * cap);
-        end[b] = (unsigned int)(b * cap) + (n > small ? n : 0u);
+        // more keys than the LDS sort holds, or keys collected by the one-pass kernel's fallback sweep (pad)
+        end[b] = (unsigned int)(b * cap) + ((n > small || (ws[b].active && ws[b].pad)) ? n : 0u);
     }
 }
 
@@ -288,40 +289,42 @@ __device__ __forceinline__ double block_canonical_butterfly(double* sm64) {
     return sm64[0];
 }
 
-template <typename T>
+template <typename T, int NT = WIDE_THREADS, int ROUND = WIDE_ROUND>
 __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, double m, double* ebuf, double* sm64) {
     // canonical order: id j -> lane (j>>2)&63, per-lane increasing; exps computed in parallel per round; the
     // next round's logits are loaded into registers before this round's ordered chain runs (a second LDS
-    // buffer to overlap the chain with the next round's exps measured no faster)
-    constexpr int PT = WIDE_ROUND / WIDE_THREADS;
+    // buffer to overlap the chain with the next round's exps measured no faster).  NT threads, ROUND ids per
+    // round staged as doubles in ebuf.
+    static_assert(ROUND % NT == 0 && ROUND % 256 == 0, "round shape");
+    constexpr int PT = ROUND / NT;
     double acc = 0.0;
     float xv[PT];
     auto load_round = [&](int base) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
-            const int j = base + u * WIDE_THREADS + (int)threadIdx.x;
+            const int j = base + u * NT + (int)threadIdx.x;
             xv[u] = j < p.V ? Elem<T>::load1(rowc, j) : 0.0f;
         }
     };
     load_round(0);
-    for (int base = 0; base < p.V; base += WIDE_ROUND) {
+    for (int base = 0; base < p.V; base += ROUND) {
         double* eb = ebuf;
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
-            const int i = u * WIDE_THREADS + (int)threadIdx.x;
+            const int i = u * NT + (int)threadIdx.x;
             const int j = base + i;
             double e = 0.0;
             if (j < p.V && !is_banned(p, j)) e = exp_canon(((double)(xv[u] + 0.0f) - m) * p.inv_temp);
             eb[i] = e;
         }
-        if (base + WIDE_ROUND < p.V) load_round(base + WIDE_ROUND);
+        if (base + ROUND < p.V) load_round(base + ROUND);
         __syncthreads();
         if (threadIdx.x < 64) {
             // groups of this round in increasing order: g = base/4 + g_local, lane = g & 63; four groups' loads
             // issued ahead of their (ordered) adds
             const int g0 = base / 4;
             int gl = ((int)threadIdx.x - g0 % 64 + 64) % 64;
-            for (; gl + 3 * 64 < WIDE_ROUND / 4; gl += 4 * 64) {
+            for (; gl + 3 * 64 < ROUND / 4; gl += 4 * 64) {
                 double t[16];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
@@ -330,7 +333,7 @@ __device__ double block_exact_row_sum(const StepParams& p, const char* rowc, dou
 #pragma unroll
                 for (int v = 0; v < 16; ++v) acc += t[v];
             }
-            for (; gl < WIDE_ROUND / 4; gl += 64) {
+            for (; gl < ROUND / 4; gl += 64) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc += eb[4 * gl + q];
             }
@@ -757,20 +760,33 @@ __device__ __forceinline__ int wave_min_int(int v) {
 
 // the LDS path for one stream whose n <= FAST_NL collected keys sit at `kin` (global or LDS, any order): sort,
 // then the canonical tail; every thread of the 512-thread block calls it
-template <typename T, bool DECODE>
+// the keys a thread loads: slot r of thread tid -- any partition of the stream's n keys over the block's slots
+// (the counting sort below does not care which thread holds which key)
+struct KeysFlat {  // one array (global memory or LDS): slot r of thread tid = key r * FAST_THREADS + tid
+    const uint64_t* k;
+    int n;
+    __device__ __forceinline__ bool operator()(int r, uint64_t& key) const {
+        const int i = r * FAST_THREADS + (int)threadIdx.x;
+        key = i < n ? k[i] : 0ull;
+        return i < n;
+    }
+};
+// INX: the exact row sum (forced, unusable bound, or an ambiguous cutoff) is computed here by the block,
+// instead of handing the stream to the list kernel (the one-pass kernel: ~1 % of stream-steps)
+template <typename T, bool DECODE, bool INX = false, typename KeyAt>
 __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w, WideStat* wsb, const int b,
-                                          const int n, const uint64_t* kin, uint64_t* keys_out, const int cap,
+                                          const int n, const KeyAt kin, uint64_t* keys_out, const int cap,
                                           unsigned int* todo, uint64_t* s_keys, uint64_t* s_aux) {
     uint32_t* s_cnt = (uint32_t*)s_aux;
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    // ---- load (unsorted, as collected) + key range
+    // ---- load (unsorted, as collected) + key range; every key is in registers before the first LDS write
     uint64_t kr[FAST_R];
+    uint32_t vm = 0u;  // bit r: slot r holds a key
     uint64_t kmax = 0ull, kmin = ~0ull;
 #pragma unroll
     for (int r = 0; r < FAST_R; ++r) {
-        const int i = r * FAST_THREADS + tid;
-        kr[r] = i < n ? kin[i] : 0ull;
-        if (i < n) {
+        if (kin(r, kr[r])) {
+            vm |= 1u << r;
             kmax = kr[r] > kmax ? kr[r] : kmax;
             kmin = kr[r] < kmin ? kr[r] : kmin;
         }
@@ -800,9 +816,8 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     uint32_t bs[FAST_R];  // bucket << 16 | slot inside the bucket
 #pragma unroll
     for (int r = 0; r < FAST_R; ++r) {
-        const int i = r * FAST_THREADS + tid;
         bs[r] = 0u;
-        if (i < n) {
+        if ((vm >> r) & 1u) {
             const uint32_t bk = min((uint32_t)((double)(hi - kr[r]) * bscale), (uint32_t)(FAST_NB - 1));
             bs[r] = (bk << 16) | atomicAdd(&s_cnt[bk], 1u);
         }
@@ -845,17 +860,14 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     int P2 = 1;
     while (P2 < n) P2 <<= 1;
 #pragma unroll
-    for (int r = 0; r < FAST_R; ++r) {
-        const int i = r * FAST_THREADS + tid;
-        if (i < n) s_keys[s_cnt[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = kr[r];
-    }
+    for (int r = 0; r < FAST_R; ++r)
+        if ((vm >> r) & 1u) s_keys[s_cnt[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = kr[r];
     __syncthreads();
     if (!bitonic) {
         // rank = bucket start + larger keys in the bucket (keys are distinct: ids are)
 #pragma unroll
         for (int r = 0; r < FAST_R; ++r) {
-            const int i = r * FAST_THREADS + tid;
-            if (i < n) {
+            if ((vm >> r) & 1u) {
                 const uint32_t bk = bs[r] >> 16;
                 const uint32_t s0 = s_cnt[bk], s1 = bk + 1 < (uint32_t)FAST_NB ? s_cnt[bk + 1] : (uint32_t)n;
                 uint32_t c = s0;
@@ -865,10 +877,8 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < FAST_R; ++r) {
-            const int i = r * FAST_THREADS + tid;
-            if (i < n) s_keys[bs[r]] = kr[r];
-        }
+        for (int r = 0; r < FAST_R; ++r)
+            if ((vm >> r) & 1u) s_keys[bs[r]] = kr[r];
         __syncthreads();
     } else {
         // bitonic network in its one-direction form (every compare-exchange puts the larger key at the lower
@@ -930,7 +940,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     const double m = (double)wkey_val(top);
     const bool want_stats = !DECODE && p.stats != nullptr;
     RowStats rs{0.0, 0.0, 0.0};
-    if ((!DECODE && p.sample) || w.exact ||
+    if ((!DECODE && p.sample) || (w.exact && !INX) ||
         (want_stats && !row_stats_from_stream(w.S_r, w.B_r, w.U_r, w.r, m, p.inv_temp, rs))) {
         defer();
         return;
@@ -940,9 +950,11 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     const double Rd = (double)R;
     const double thr = 1.0 / Rd;
     double* s_e = (double*)s_keys;
+    bool exact = w.exact != 0;
+    double S_used = w.S_fast;
     // ---- 1. cutoff k0 (the fast-sum interval decides it, or the stream needs the exact sum)
     int fb = Kc, fa = Kc;
-    {
+    if (!exact) {
         const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15));
         const double inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
 #pragma unroll
@@ -971,6 +983,34 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         fb = min(fb, s_i[i]);
         fa = min(fa, s_i[FAST_WAVES + i]);
     }
+    if (INX && (exact || fa < fb)) {
+        // the canonical exact row sum by this block (s_keys is scratch: e_i are recomputed from the registers)
+        __syncthreads();
+        const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+        const double S = block_exact_row_sum<T, FAST_THREADS, 4096>(p, rowc, m, (double*)s_keys, (double*)(s_aux + 512));
+        exact = true;
+        S_used = S;
+        fb = Kc;
+#pragma unroll
+        for (int r = 0; r < FAST_R; ++r) {
+            const int i = r * FAST_THREADS + tid;
+            if (i < Kc) {
+                const double e = exp_canon(((double)wkey_val(ks[r]) - m) * p.inv_temp);
+                s_e[i] = e;
+                if (e / S < thr) fb = min(fb, i);
+            }
+        }
+        fb = wave_min_int(fb);
+        if (lane == 0) s_i[wv] = fb;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) fb = min(fb, s_i[i]);
+        fa = Kc;
+    }
+#if NSG_SCAN_DIAG == 4  // timing diagnostics: up to the cutoff
+    if (tid == 0) atomicExch((unsigned int*)&keys_out[(int64_t)b * cap], (unsigned int)(fb + fa));
+    return;
+#endif
     int k = fb < 2 ? 2 : fb;
     if (k > p.topk) k = p.topk;
     // ambiguous cutoff (the exact row sum: measured cheaper in the list kernel than in this one, whose
@@ -1118,7 +1158,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         kl = 0.0;
         for (int i = 0; i < FAST_WAVES; ++i) kl += s_d[8 + i];
     }
-    wide_finish<DECODE>(p, b, st, k, kp, sel, false, w.S_fast, s_c[1], s_c[2], shift, (uint64_t)s_c[3], m, rs, kl,
+    wide_finish<DECODE>(p, b, st, k, kp, sel, exact, S_used, s_c[1], s_c[2], shift, (uint64_t)s_c[3], m, rs, kl,
                         want_stats);
 }
 
@@ -1387,7 +1427,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_sc
 #endif
     if (n <= FAST_NL) {
         if (tid == 0) count[b] = (unsigned int)n;
-        fast_tail<T, DECODE>(p, w, &ws[b], b, n, s_keys, keys_out, cap, todo, s_keys, s_aux);
+        fast_tail<T, DECODE>(p, w, &ws[b], b, n, KeysFlat{s_keys, n}, keys_out, cap, todo, s_keys, s_aux);
         return;
     }
     __syncthreads();
@@ -1398,6 +1438,525 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_sc
         count[b] = (unsigned int)n;
         todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
     }
+}
+
+// ------------------------------------------------------------------------------------------ one-pass wide step
+// (round 3) The row is streamed ONCE.  wide_scan_kernel needed two sweeps because the collection threshold
+// x_t = r + T ln(S_r / R) (an id below it has e_i < S/R: below the cutoff for certain) depends on the row sum S,
+// known only after the first sweep.  But any partial sum is a lower bound of S, so a threshold computed from the
+// ids seen so far is a valid (lower, i.e. collect-more) threshold, and it only rises as the sweep goes on:
+//   * each of the 8 waves takes a contiguous slice of the row; its last NSW tiles (8 x NSW x 1 KiB = 4,096 ids,
+//     a stratified sample) are read first; their max is the reference r and their sum the first threshold;
+//   * the wave streams the rest of its slice (non-temporal 16-B loads, a ring of NR tiles refilled in place),
+//     accumulating the fast sum (fp32 per tile, float64 across tiles), e * |arg| for the data-dependent bound,
+//     the lane's top two values, and appending the ids at or above its threshold to its own LDS buffer
+//     (704 keys; when full, compacted to the current threshold -- ids below it are below the final one too);
+//   * after every ring group the wave publishes its partial sum and re-reads the others' (plain LDS words:
+//     each is a partial sum, so whatever subset is read is a lower bound), and raises its threshold;
+//   * ids that can be among the top two are kept too (k >= 2): a wave's threshold is min(x_t, its running
+//     second max), which never exceeds the row's second max when that id arrives.
+// At the end the buffers are filtered to x >= min(x_t(final interval), m2) -- exactly a prefix of the ranking --
+// merged into one LDS array and handed to fast_tail.  A wave whose buffer overflows even after compaction makes
+// the stream take the old path: one more block sweep collects into global memory (sorted in LDS by fast_tail
+// when it fits, else by the device-wide sort and the list kernel).
+#ifndef NSG_WIDE_ONEPASS
+#define NSG_WIDE_ONEPASS 1
+#endif
+#ifndef NSG_OP_RING
+#define NSG_OP_RING 4
+#endif
+constexpr int OP_CAPW = FAST_NL / FAST_WAVES;  // keys per wave buffer
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v += __uint_as_float(xor_lane_u32<32>(__float_as_uint(v)));
+    v += __uint_as_float(xor_lane_u32<16>(__float_as_uint(v)));
+    v += __uint_as_float(xor_lane_u32<8>(__float_as_uint(v)));
+    v += __uint_as_float(xor_lane_u32<4>(__float_as_uint(v)));
+    v += __uint_as_float(xor_lane_u32<2>(__float_as_uint(v)));
+    v += __uint_as_float(xor_lane_u32<1>(__float_as_uint(v)));
+    return v;
+}
+// wave top two of the lanes' (m1, m2): every lane ends with the wave's (m1, m2)
+__device__ __forceinline__ void wave_top2(float& m1, float& m2) {
+    auto step = [&](float o1, float o2) __attribute__((always_inline)) {
+        m2 = fmaxf(fminf(m1, o1), fmaxf(m2, o2));
+        m1 = fmaxf(m1, o1);
+    };
+    step(__uint_as_float(xor_lane_u32<32>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<32>(__float_as_uint(m2))));
+    step(__uint_as_float(xor_lane_u32<16>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<16>(__float_as_uint(m2))));
+    step(__uint_as_float(xor_lane_u32<8>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<8>(__float_as_uint(m2))));
+    step(__uint_as_float(xor_lane_u32<4>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<4>(__float_as_uint(m2))));
+    step(__uint_as_float(xor_lane_u32<2>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<2>(__float_as_uint(m2))));
+    step(__uint_as_float(xor_lane_u32<1>(__float_as_uint(m1))), __uint_as_float(xor_lane_u32<1>(__float_as_uint(m2))));
+}
+
+// raw buffer entries of the one-pass kernel: value bits << 32 | id (the order transform waits for the tail)
+__device__ __forceinline__ uint64_t op_raw(float x, uint32_t j) { return ((uint64_t)__float_as_uint(x) << 32) | j; }
+__device__ __forceinline__ float op_raw_val(uint64_t e) { return __uint_as_float((uint32_t)(e >> 32)); }
+__device__ __forceinline__ uint64_t op_raw_key(uint64_t e) { return wkey(op_raw_val(e), (uint32_t)e); }
+// keep the entries of a wave buffer whose value is >= t, in place and in order
+__device__ __forceinline__ int wave_compact(uint64_t* wbuf, int cnt, float t) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    int nc = 0;
+    for (int base = 0; base < cnt; base += WAVE) {
+        const int i = base + lane;
+        const uint64_t k = i < cnt ? wbuf[i] : 0ull;
+        const bool keep = i < cnt && op_raw_val(k) >= t;
+        const uint64_t km = ballot(keep);
+        if (keep) wbuf[nc + lanes_below(km)] = k;
+        nc += popc64(km);
+    }
+    return __builtin_amdgcn_readfirstlane(nc);
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_onepass_kernel(
+    StepParams p, WideStat* ws, uint64_t* keys_in, uint64_t* keys_out, unsigned int* count, int cap,
+    unsigned int* todo) {
+    __shared__ uint64_t s_keys[FAST_NL];
+    __shared__ uint64_t s_aux[FAST_NB / 2];
+    constexpr int W = Elem<T>::W;
+    constexpr int TS = WAVE * W;             // ids per wave tile (1 KiB)
+    constexpr int NSW = (W == 4) ? 2 : 1;    // sample tiles per wave: 8 x NSW x TS = 4,096 ids
+    constexpr int NR = NSG_OP_RING;
+    const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & (WAVE - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    const ns_stream_state st = p.state[b];
+    bool active = !(st.flags & NS_ST_DONE);
+    if (!DECODE && !p.sample && active && st.bit_pos >= p.nbits[b]) {
+        if (tid == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
+        active = false;
+    }
+    if (DECODE && p.active && !p.active[b]) active = false;
+    if (!active) {
+        if (tid == 0) {
+            ws[b].active = 0;
+            count[b] = 0;
+        }
+        return;
+    }
+    const int V = p.V;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int ntiles = (V + TS - 1) / TS;
+    const int per = (ntiles + FAST_WAVES - 1) / FAST_WAVES;
+    const int s0 = min(ntiles, wv * per), s1 = min(ntiles, s0 + per);
+    const int ns = min(NSW, s1 - s0);  // sample tiles: the last ns tiles of the slice
+    const int se = s1 - ns;            // streamed tiles [s0, se)
+    uint64_t* wbuf = s_keys + wv * OP_CAPW;
+    // LDS scratch (s_aux, 64-bit words): [0,4) published partial sums (f32), [8,12) wave maxima (f32),
+    // [16,48) per-wave double sums, [48,52) counts, [52,56) running thresholds, [60] sweep counter
+    volatile float* s_part = (volatile float*)(s_aux + 0);
+    float* s_m1 = (float*)(s_aux + 8);
+    double* s_d = (double*)(s_aux + 16);
+    int* s_n = (int*)(s_aux + 48);
+    float* s_xt = (float*)(s_aux + 52);
+    const bool stats = p.stats != nullptr;
+    const double temp = 1.0 / p.inv_temp;
+    const float tempf = (float)temp;
+    const double Rd = (double)(st.hi - st.lo);
+    const float lnthr = (float)(-log(Rd));  // ln(1/R)
+
+    // x of tile t: out-of-row and banned ids -> -1e30 (no sum, below every real max), and bit q of `mb` set (never
+    // collected: a real -inf logit IS collected when the threshold is -inf).  Bans are walked with a per-wave pointer
+    // (`bi`, `next_ban`: the first ban at or after the tiles still to come), so the per-tile test is one scalar
+    // compare; tiles must be visited in increasing order between resets of the pointer.
+    int bi = 0, next_ban = 0x7FFFFFFF;
+    auto ban_reset = [&](int t) __attribute__((always_inline)) {
+        bi = 0;
+        while (bi < p.nbanned && p.banned[bi] < t * TS) ++bi;
+        next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+    };
+    auto load_x = [&](int t, const uint4& raw, float (&x)[W], uint32_t& mb) __attribute__((always_inline)) {
+        Elem<T>::unpack(raw, x);
+        mb = 0u;
+        const int j0 = t * TS + lane * W;
+        if ((t + 1) * TS > V) {
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (j0 + q >= V) {
+                    x[q] = -1.0e30f;
+                    mb |= 1u << q;
+                }
+        }
+        while (next_ban < (t + 1) * TS) {  // wave-uniform, at most nbanned times per slice
+            const int d = next_ban - j0;
+            if (d >= 0 && d < W) {
+#pragma unroll
+                for (int q = 0; q < W; ++q)
+                    if (q == d) {
+                        x[q] = -1.0e30f;
+                        mb |= 1u << q;
+                    }
+            }
+            ++bi;
+            next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+        }
+    };
+    float r = 0.0f, nrc = 0.0f;  // reference and -fl(r * c32)
+    float m1 = -__builtin_inff();
+    double accS = 0.0, accT = 0.0, accB = 0.0, accU = 0.0;
+    float accSf = 0.0f;
+    // one tile's fast-sum terms: e = 2^fma(x, c32, -r c32) in packed pairs, sum e and sum e*t (the bound's B_t),
+    // flushed into float64 per tile (W terms per fp32 partial); the lane max with v_max3.  Masked ids are -1e30
+    // (t finite, e = 0, e*t = 0); a real -inf logit makes B_t NaN, i.e. the bound unusable (exact row sum).
+    auto sum_tile = [&](const float (&x)[W]) __attribute__((always_inline)) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 c2 = {p.c32, p.c32}, n2 = {nrc, nrc};
+        f2 a2 = {0.0f, 0.0f}, b2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < W; q += 2) {
+            const f2 x2 = {x[q], x[q + 1]};
+            const f2 t = __builtin_elementwise_fma(x2, c2, n2);
+            const f2 e2 = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            a2 += e2;
+            b2 = __builtin_elementwise_fma(e2, t, b2);
+            m1 = __builtin_fmaxf(__builtin_fmaxf(m1, x[q]), x[q + 1]);  // v_max3_f32
+        }
+        const float a = a2.x + a2.y;
+        accS += (double)a;
+        accT += (double)(b2.x + b2.y);
+        accSf += a;
+        if (stats) {  // sum e*(x-r) and the untempered sum: the statistics, not the bound
+            float bb = 0.0f, uu = 0.0f;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const float dx = fmaxf(x[q] - r, -3.0e38f);
+                const float e = __builtin_amdgcn_exp2f(dx * p.c32);
+                bb += e * dx;
+                uu += __builtin_amdgcn_exp2f(dx * L2E_F);
+            }
+            accB += (double)bb;
+            accU += (double)uu;
+        }
+    };
+    int cnt = 0;          // keys in this wave's buffer (wave-uniform)
+    bool ovf = false;     // the buffer overflowed even after compaction (wave-uniform)
+    float t_wave = -__builtin_inff();  // candidate threshold (wave-uniform)
+    auto compact = [&]() __attribute__((always_inline)) { cnt = wave_compact(wbuf, cnt, t_wave); };
+    // appends: each lane's passing values go to consecutive slots (lane order, then value order inside the
+    // lane): a per-lane count, one wave scan (DPP), predicated raw writes -- no per-value ballot/mbcnt
+    auto append_tile = [&](int t, const float (&x)[W], uint32_t mb) __attribute__((always_inline)) {
+#if defined(NSG_OP_NOAPPEND)  // timing diagnostics: streaming and sums only
+        return;
+#endif
+        uint32_t c = 0u;
+#pragma unroll
+        for (int q = 0; q < W; ++q) c += (x[q] >= t_wave) ? 1u : 0u;
+        if (mb) {  // masked values (tail tile / banned ids) never pass: recount without them (rare)
+            c = 0u;
+#pragma unroll
+            for (int q = 0; q < W; ++q) c += (x[q] >= t_wave && !((mb >> q) & 1u)) ? 1u : 0u;
+        }
+        const uint32_t incl = wave_incl_scan_u32(c);
+        const int tot = __builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        if (tot == 0 || ovf) return;
+        if (cnt + tot > OP_CAPW) {
+            compact();
+            if (cnt + tot > OP_CAPW) {
+                ovf = true;
+                return;
+            }
+        }
+        uint32_t pos = (uint32_t)cnt + incl - c;
+        const uint32_t j0 = (uint32_t)(t * TS + lane * W);
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            if (x[q] >= t_wave && !((mb >> q) & 1u)) wbuf[pos++] = op_raw(x[q], j0 + q);
+        cnt += tot;
+    };
+    // threshold from a lower bound S_part of the row sum against r (fp32; 2^-10 of slack covers every rounding
+    // of the partial sum by orders of magnitude, and the widening every rounding of the threshold)
+    auto threshold = [&](float s_part, float mx) __attribute__((always_inline)) -> float {
+        if (p.sample) {  // sampler support e_i >= 2^-60 of the max: any running max is a lower bound of m
+            const float t = mx - tempf * 41.58883083359672f;
+            return t - 1.0e-4f * (1.0f + fabsf(mx) + tempf * 41.58883083359672f);
+        }
+        if (!(s_part > 0.0f && s_part < 3.0e38f)) return -__builtin_inff();
+        const float L = __builtin_amdgcn_logf(s_part * 0.9990234375f) * 0.6931471805599453f + lnthr;
+        const float t = r + tempf * L;
+        return t - 1.0e-4f * (1.0f + fabsf(r) + fabsf(tempf * L));
+    };
+    float xt_run = -__builtin_inff();
+
+    // ---- sample tiles first (and the first ring tiles in flight behind them)
+    uint4 smp[NSW];
+#pragma unroll
+    for (int i = 0; i < NSW; ++i)
+        if (i < ns) smp[i] = rd.vec((se + i) * WAVE + lane);
+    uint4 ring[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+        if (s0 + j < se) ring[j] = rd.vec((s0 + j) * WAVE + lane);
+    float xs[NSW][W];
+    uint32_t mbs[NSW];
+    float smax = -__builtin_inff();
+    ban_reset(se);
+#pragma unroll
+    for (int i = 0; i < NSW; ++i) {
+        mbs[i] = ~0u;
+#pragma unroll
+        for (int q = 0; q < W; ++q) xs[i][q] = -1.0e30f;
+        if (i < ns) {
+            load_x(se + i, smp[i], xs[i], mbs[i]);
+#pragma unroll
+            for (int q = 0; q < W; ++q) smax = fmaxf(smax, xs[i][q]);
+        }
+    }
+    smax = wave_max(smax);
+    if (lane == 0) s_m1[wv] = smax;
+    __syncthreads();
+    r = s_m1[0];
+#pragma unroll
+    for (int i = 1; i < FAST_WAVES; ++i) r = fmaxf(r, s_m1[i]);
+    if (!(r > -1.0e29f)) r = 0.0f;  // no valid id in the sample
+    r = uni_f32(r);
+    nrc = uni_f32(-(r * p.c32));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NSW; ++i)
+        if (i < ns) sum_tile(xs[i]);
+    {
+        const float ws0 = wave_sum_f32(accSf);
+        if (lane == 0) s_part[wv] = ws0;
+        __syncthreads();
+        float tot = 0.0f;
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) tot += s_part[i];
+        xt_run = uni_f32(threshold(tot, r));
+        t_wave = xt_run;
+    }
+#pragma unroll
+    for (int i = 0; i < NSW; ++i)
+        if (i < ns) append_tile(se + i, xs[i], mbs[i]);
+
+    // ---- stream the rest of the slice; the threshold rises every UPD tiles (16 values per lane)
+    constexpr int UPD = 16 / W;
+    static_assert(NR % UPD == 0, "ring a multiple of the update interval");
+    ban_reset(s0);
+    for (int base = s0; base < se; base += NR) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int t = base + j;
+            if (t < se) {
+                const uint4 v = ring[j];
+                if (t + NR < se) ring[j] = rd.vec((t + NR) * WAVE + lane);
+                float x[W];
+                uint32_t mb;
+                load_x(t, v, x, mb);
+                sum_tile(x);
+                append_tile(t, x, mb);
+            }
+#if !defined(NSG_OP_NOUPDATE)
+            if ((j + 1) % UPD == 0 && t < se) {
+                // publish this wave's partial sum, read the others' (each a partial sum: whatever is read is a
+                // lower bound of the row sum), raise the threshold
+                const float wsum = wave_sum_f32(accSf);
+                if (lane == 0) s_part[wv] = wsum;
+                float tot = 0.0f;
+#pragma unroll
+                for (int i = 0; i < FAST_WAVES; ++i) tot += s_part[i];
+                xt_run = uni_f32(fmaxf(xt_run, threshold(tot, p.sample ? wave_max(m1) : r)));
+                t_wave = xt_run;
+            }
+#endif
+        }
+    }
+#if defined(NSG_OP_DIAG) && NSG_OP_DIAG == 1  // register-pressure / timing diagnostics: streaming only
+    if (lane == 0) s_part[wv] = (float)accS + accSf + (float)accT + m1 + (float)cnt;
+    if (tid == 0) count[b] = 0u;
+    return;
+#endif
+
+    // ---- the row's statistics
+    accS = wave_sum_butterfly(accS);
+    accT = wave_sum_butterfly(accT);
+    if (stats) {
+        accB = wave_sum_butterfly(accB);
+        accU = wave_sum_butterfly(accU);
+    }
+    m1 = wave_max(m1);
+    __syncthreads();  // every wave is past its last read of s_part
+    if (lane == 0) {
+        s_d[wv] = accS;
+        s_d[FAST_WAVES + wv] = accT;
+        s_d[2 * FAST_WAVES + wv] = accB;
+        s_d[3 * FAST_WAVES + wv] = accU;
+        s_m1[wv] = m1;
+        s_n[wv] = ovf ? -1 : cnt;
+        s_xt[wv] = xt_run;
+    }
+    __syncthreads();
+    double S_r = 0.0, T_r = 0.0, B_r = 0.0, U_r = 0.0;
+    float bm1 = -__builtin_inff(), xt_all = -__builtin_inff();
+    bool any_ovf = false;
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) {
+        S_r += s_d[i];
+        T_r += s_d[FAST_WAVES + i];
+        B_r += s_d[2 * FAST_WAVES + i];
+        U_r += s_d[3 * FAST_WAVES + i];
+        bm1 = fmaxf(bm1, s_m1[i]);
+        xt_all = fmaxf(xt_all, s_xt[i]);  // every wave collected all ids >= its own final threshold
+        any_ovf |= s_n[i] < 0;
+    }
+    if (!(bm1 > -1.0e29f)) bm1 = -__builtin_inff();
+    WideStat w;
+    {
+        double Sf = 0.0, S_lo = 0.0, S_hi = 0.0;
+        const bool ok = fast_sum_interval_dd(uni_f64(S_r), uni_f64(T_r), r, (double)(bm1 + 0.0f), p.c32, p.inv_temp,
+                                             W, Sf, S_lo, S_hi);
+        w.m = uni_f32(bm1);
+        w.m2 = -__builtin_inff();  // not tracked (k >= 2 is checked below)
+        w.r = r;
+        w.active = 1;
+        w.S_lo = uni_f64(S_lo);
+        w.S_hi = uni_f64(S_hi);
+        w.S_fast = uni_f64(Sf);
+        w.exact = (uint32_t)__builtin_amdgcn_readfirstlane((ok && !(p.flags & NS_STEP_FORCE_EXACT_SUM)) ? 0 : 1);
+        w.pad = 0;
+        w.S_r = uni_f64(S_r);
+        w.B_r = uni_f64(B_r);
+        w.U_r = uni_f64(U_r);
+        // the final collection threshold (as wide_collect_kernel), never below what every wave collected
+        float xt = -__builtin_inff();
+        const double thr = 1.0 / Rd;
+        if (p.sample) {
+            const double t = (double)w.m - temp * 41.58883083359672;
+            xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + temp * 41.58883083359672));
+        } else if (ok) {
+            const double L = log(S_lo * thr);
+            const double t = (double)w.m + temp * L;
+            xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + fabs(temp * L)));
+        }
+        xt_all = uni_f32(fmaxf(xt, xt_all));  // ids >= it: a prefix of the ranking, all collected
+    }
+    if (tid == 0) ws[b] = w;
+    __syncthreads();
+    // the row's second largest valid value (a block rescan of the row; block-uniform result)
+    auto top2_second = [&]() __attribute__((always_inline)) -> float {
+        float l1 = -__builtin_inff(), l2 = -__builtin_inff();
+        ban_reset(wv);
+        for (int t0 = 0; t0 < ntiles; t0 += FAST_WAVES) {
+            const int t = t0 + wv;
+            if (t < ntiles) {
+                float x[W];
+                uint32_t mb;
+                load_x(t, rd.vec(t * WAVE + lane), x, mb);
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    const float v = ((mb >> q) & 1u) ? -__builtin_inff() : x[q];
+                    l2 = fmaxf(l2, fminf(l1, v));
+                    l1 = fmaxf(l1, v);
+                }
+            }
+        }
+        wave_top2(l1, l2);
+        __syncthreads();
+        if (lane == 0) {
+            s_m1[wv] = l1;
+            s_xt[wv] = l2;
+        }
+        __syncthreads();
+        float b1 = -__builtin_inff(), b2 = -__builtin_inff();
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) {
+            b2 = fmaxf(fminf(b1, s_m1[i]), fmaxf(b2, s_xt[i]));
+            b1 = fmaxf(b1, s_m1[i]);
+        }
+        __syncthreads();
+        return uni_f32(b2);
+    };
+    // one block sweep collecting the valid ids with x >= thr into this stream's global key segment; the count
+    uint32_t* s_ctr = (uint32_t*)(s_aux + 60);
+    uint64_t* kout = keys_in + (int64_t)b * cap;
+    auto sweep_global = [&](float thr) __attribute__((always_inline)) -> uint32_t {
+        __syncthreads();
+        if (tid == 0) s_ctr[0] = 0u;
+        __syncthreads();
+        ban_reset(wv);
+        for (int t0 = 0; t0 < ntiles; t0 += FAST_WAVES) {
+            const int t = t0 + wv;
+            if (t < ntiles) {
+                float x[W];
+                uint32_t mb;
+                load_x(t, rd.vec(t * WAVE + lane), x, mb);
+                uint32_t tot = 0;
+#pragma unroll
+                for (int q = 0; q < W; ++q) tot += (uint32_t)popc64(ballot(x[q] >= thr && !((mb >> q) & 1u)));
+                if (tot) {
+                    uint32_t bs = 0u;
+                    if (lane == 0) bs = atomicAdd(s_ctr, tot);
+                    bs = (uint32_t)__builtin_amdgcn_readfirstlane((int)bs);
+                    const int j0 = t * TS + lane * W;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        const bool take = x[q] >= thr && !((mb >> q) & 1u);
+                        const uint64_t mk = ballot(take);
+                        const uint32_t pos = bs + (uint32_t)lanes_below(mk);
+                        if (take && pos < (uint32_t)cap) kout[pos] = wkey(x[q], (uint32_t)(j0 + q));
+                        bs += (uint32_t)popc64(mk);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t got = min(s_ctr[0], (uint32_t)cap);
+        __syncthreads();
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+    };
+
+    int n = 0;
+    bool from_lds = false;
+    if (!any_ovf) {
+        // ---- each wave filters its buffer to x >= xt_all in place; fast_tail reads the kept keys of its own
+        // wave's buffer (slot r of a thread = entry r * 64 + lane; every key in registers before it writes LDS)
+        t_wave = xt_all;
+        compact();
+        if (lane == 0) s_n[wv] = cnt;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FAST_WAVES; ++i) n += s_n[i];
+        __syncthreads();
+        from_lds = n >= 2 || n >= V - p.nbanned;
+        // fewer than two ids clear the threshold (a peaked row: k >= 2 needs the second largest, which the
+        // running threshold may have skipped): collect down to it with a sweep (rare)
+        if (!from_lds) xt_all = uni_f32(fminf(xt_all, top2_second()));
+    }
+    if (!from_lds) {
+        // ---- a buffer overflowed (or the top two are needed): one block sweep collects x >= xt_all into the
+        // stream's global key segment; the LDS sort takes it from there when it fits, else the device-wide sort
+        // (ws.pad marks it for wide_offsets_kernel) and the list kernel
+        uint32_t got = sweep_global(xt_all);
+        if (got < 2u && (int)got < V - p.nbanned) {  // overflowed AND peaked: the top two are below the threshold
+            xt_all = uni_f32(fminf(xt_all, top2_second()));
+            got = sweep_global(xt_all);
+        }
+        if (tid == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 1], 1ull);
+        if (got > (uint32_t)FAST_NL) {
+            if (tid == 0) {
+                count[b] = got;
+                ws[b].pad = 1u;
+                todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
+            }
+            return;
+        }
+        n = (int)got;
+    }
+    if (tid == 0) count[b] = (unsigned int)n;
+    static_assert(FAST_R * WAVE == OP_CAPW, "one slot per buffer entry");
+    const int mine = cnt;
+    auto at = [&](int rr, uint64_t& key) __attribute__((always_inline)) -> bool {
+        if (from_lds) {  // block-uniform
+            const int j = rr * WAVE + lane;
+            key = j < mine ? op_raw_key(wbuf[j]) : 0ull;
+            return j < mine;
+        }
+        const int i = rr * FAST_THREADS + tid;
+        key = i < n ? kout[i] : 0ull;
+        return i < n;
+    };
+    fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, at, keys_out, cap, todo, s_keys, s_aux);
 }
 
 // ------------------------------------------------------------------------------------------ rank coder
@@ -1661,8 +2220,13 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     NsgWide& w = ctx->wide;
     const int B = p.B;
     if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
+#if NSG_WIDE_ONEPASS
+    hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
+                       w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+#else
     hipLaunchKernelGGL((nsg::wide_scan_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+#endif
     hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
                        w.count, w.begin, w.end, (unsigned int)nsg::FAST_NL, nullptr);
     size_t bytes = w.sort_tmp_bytes;

@@ -162,40 +162,78 @@ def test_cover_text_round_trip_gpu_provider(finish_sent):
     assert cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm) == secrets
 
 
+class CharMergeTokenizer:
+    """BPE-style test tokenizer over 64 ids: 'a'-'z', 'A'-'Z', '-', four digits, six two-letter merges ("th",
+    "he", "in", "er", "an", "re": ids 57-62) and <|endoftext|> (63).  ``encode`` is greedy longest match, so a
+    cover whose coder emitted 't', 'h' re-tokenises to the merge "th".  The provider bans the merges (and the
+    end of text), so the coder only ever emits single characters and every merge in a re-tokenised text is a
+    BPE artefact that the reference's repair (code_base/arithmetic.py:300-342) undoes: the only kept candidate
+    whose text is a prefix of "th" is "t"."""
+
+    MERGES = ["th", "he", "in", "er", "an", "re"]
+
+    def __init__(self):
+        import string
+
+        # no whitespace piece: spans_to_text strips the cover (textio.py:37-55), which would drop a trailing one
+        self.pieces = list(string.ascii_lowercase) + list(string.ascii_uppercase) + ["-"] + list("0123")
+        self.pieces += self.MERGES + ["<|endoftext|>"]
+        assert len(self.pieces) == 64
+        self.lookup = {p: i for i, p in enumerate(self.pieces)}
+        self.eos_id = 63
+
+    def banned(self):
+        return [63] + [self.lookup[m] for m in self.MERGES]
+
+    def decode(self, ids):
+        return "".join(self.pieces[int(i)] for i in ids)
+
+    def encode(self, text, add_special_tokens=False):
+        out, i = [], 0
+        while i < len(text):
+            if text.startswith("<|endoftext|>", i):
+                out.append(63)
+                i += len("<|endoftext|>")
+                continue
+            two = self.lookup.get(text[i:i + 2])
+            if two is not None and i + 2 <= len(text):
+                out.append(two)
+                i += 2
+            elif text[i] in self.lookup:
+                out.append(self.lookup[text[i]])
+                i += 1
+            else:
+                i += 1  # unknown character: dropped
+        return out
+
+
 def test_cover_text_reveal_with_bpe_repair():
-    """Cover TEXT whose re-tokenisation differs from the emitted ids (a greedy longest-match toy tokenizer
-    merges adjacent pieces, also across span boundaries): texts_to_spans repairs the received ids while
-    decoding (code_base/arithmetic.py:300-342 via decode_counted_repair) and the secrets come back.  Covers that
-    re-tokenise exactly must all reveal; covers that do not must reveal too wherever the reference's heuristic
-    repairs every merge (the test requires most of them, and at least one)."""
+    """Cover TEXT whose re-tokenisation differs from the emitted ids (greedy merges, within spans and across
+    span boundaries): texts_to_spans repairs the received ids while decoding (code_base/arithmetic.py:233-242,
+    300-342 via decode_counted_repair) and every secret comes back -- also those whose covers re-tokenise
+    differently."""
     from neuralsteganography_amd.codec.textio import seed_to_ids, spans_to_text
     from neuralsteganography_amd.cover import cover_reveal_batch
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
     from neuralsteganography_amd.stego import stego_encode_batch
-    from tests.golden.toy_tokenizer import ToyTokenizer
 
-    V = 700
-    tok = ToyTokenizer(V)
-    m = random_gpt2("tiny", vocab_size=V, n_positions=1024, seed=29)
-    lm = HipArithmeticLM(m, tok, compute_dtype=torch.float32)
+    tok = CharMergeTokenizer()
+    # fp16 compute: the batch-invariant native decode step, so a cover decodes at any batch size (fp32 compute
+    # keeps PyTorch's GEMMs, whose results depend on the batch: decode would need the encoder's composition)
+    m = random_gpt2("tiny", vocab_size=64, n_positions=2048, n_embd=128, n_head=2, seed=29)
+    lm = HipArithmeticLM(m, tok, banned=tok.banned())
     q = {"temp": 1.0, "precision": 26, "topk": 300, "finish_sent": False}
     secrets = [synthetic.payload_bytes(s, 5 + 7 * s) for s in range(12)]
-    seed = "abc"
+    seed = "Abc"
     res = stego_encode_batch(secrets, chunk_bytes=24, ecc="none", quality=q, seed_text=seed, lm=lm)
     seed_ids = seed_to_ids(seed, tok)
     texts, differs = [], []
     for r in res:
+        assert all(t not in tok.banned() for s in r for t in s)
         text = spans_to_text([list(s) for s in r], seed_ids, tok)
         texts.append(text)
-        emitted = seed_ids + [t for s in r for t in s]
-        differs.append(tok.encode(text) != emitted)
-    assert any(differs), "no cover re-tokenises differently: pick another seed"
-    got = cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm, return_errors=True)
-    for i, (g, d) in enumerate(zip(got, differs)):
-        if not d:
-            assert g == secrets[i], f"cover {i} re-tokenises exactly but did not reveal"
-    repaired = [i for i, d in enumerate(differs) if d and got[i] == secrets[i]]
-    n_diff = sum(differs)
-    print(f"BPE reveal: {n_diff} of {len(texts)} covers re-tokenise differently, {len(repaired)} revealed")
-    assert repaired and len(repaired) * 2 >= n_diff
+        differs.append(tok.encode(text) != seed_ids + [t for s in r for t in s])
+    assert sum(differs) >= 3, "too few covers re-tokenise differently: pick another seed"
+    got = cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm)
+    assert got == secrets

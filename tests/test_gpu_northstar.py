@@ -137,7 +137,8 @@ class _IdTokenizer:
 @pytest.mark.timeout(900)
 def test_c5_like_gpt2_medium_topk100_guard_on_1024_secrets():
     from neuralsteganography_amd.cover import (_ensure_guard, cover_generate_batch, cover_reveal_batch,
-                                               prepare_gate_thresholds)
+                                               iter_attempts, prepare_gate_thresholds)
+    from neuralsteganography_amd.stego import normalise_quality
     from neuralsteganography_amd.exceptions import QualityGateError
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
@@ -155,15 +156,29 @@ def test_c5_like_gpt2_medium_topk100_guard_on_1024_secrets():
     guard = _ensure_guard(None)
     ppl = sorted(v.metrics["ppl"] for v in guard.evaluate_batch(first, prepare_gate_thresholds(None)))
     gate = {"max_ppl": float(ppl[n // 2])}
+    # the reference's schedule (api.py:496-523: top_k 80 / 70, temp 0.8 / 0.7) with a seed pool the test
+    # tokenizer can spell, so that each cover's text tells which attempt made it
+    strategy = {"seed_pool": ["w21. w22. w23", "w31. w32. w33"]}
     out = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=True,
-                               gate_thresholds=gate, regen_attempts=2, return_errors=True)
+                               gate_thresholds=gate, regen_attempts=2, regen_strategy=strategy, return_errors=True)
     passed = [i for i, t in enumerate(out) if isinstance(t, str)]
     failed = [i for i, t in enumerate(out) if isinstance(t, QualityGateError)]
     assert len(passed) + len(failed) == n
     assert passed and failed, (len(passed), len(failed), gate)
     for i in failed:
         assert out[i].reasons  # rejected by the last attempt of the schedule, with its reasons
-    got = cover_reveal_batch([out[i] for i in passed], seed_text=seed, quality=q, ecc="rs", lm=lm)
-    wrong = [i for i, g in zip(passed, got) if g != secrets[i]]
-    assert not wrong, f"{len(wrong)} of {len(passed)} passed covers did not reveal (first: {wrong[:8]})"
-    print(f"C5-like: {n} secrets, gate {gate}, {len(passed)} passed the guard and revealed, {len(failed)} rejected")
+    # a cover reveals with the seed and quality of the attempt that made it (as in the reference, cover_reveal
+    # takes them from the caller)
+    attempts = list(iter_attempts(seed, 2, strategy))
+    by_attempt = {}
+    for i in passed:
+        a = next(j for j, att in enumerate(attempts) if out[i].startswith(att.seed_text))
+        by_attempt.setdefault(a, []).append(i)
+    assert 0 in by_attempt, {a: len(v) for a, v in by_attempt.items()}
+    for a, idx in sorted(by_attempt.items()):
+        aq = dict(normalise_quality(q), **attempts[a].overrides)
+        got = cover_reveal_batch([out[i] for i in idx], seed_text=attempts[a].seed_text, quality=aq, ecc="rs", lm=lm)
+        wrong = [i for i, g in zip(idx, got) if g != secrets[i]]
+        assert not wrong, f"attempt {a + 1}: {len(wrong)} of {len(idx)} covers did not reveal (first: {wrong[:8]})"
+    print(f"C5-like: {n} secrets, gate {gate}, passed and revealed per attempt "
+          f"{ {a + 1: len(v) for a, v in sorted(by_attempt.items())} }, {len(failed)} rejected")

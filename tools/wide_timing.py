@@ -49,7 +49,9 @@ def main():
     torch.cuda.synchronize()
     ms = float(np.mean([x.elapsed_time(y) for x, y in ev]))
     sess.raise_errors()
-    print(json.dumps({"lib": Path(_lib.LIB_PATH).name, "batch": B, "topk": a.topk, "precision": a.precision,
+    c1 = ctx.counters()
+    print(json.dumps({"lib": Path(_lib.LIB_PATH).name, "batch": B, "topk": a.topk, "precision": a.precision, "dtype": a.dtype,
+                      "counters": [x - y for x, y in zip(c1, c0)],
                       "ms_per_step": round(ms, 4), "tokens": int(sess.fields()["ntokens"].sum()),
                       "exact_sum_steps": ctx.counters()[0] - c0[0], "stream_steps": B * a.steps}), flush=True)
 
