@@ -179,6 +179,14 @@ def probs_to_logits(rows: np.ndarray) -> np.ndarray:
     return lg.astype(np.float32)
 
 
+def _declared_vocab(provider) -> int:
+    for name in ("vocab_size", "n_vocab", "vocab"):
+        v = getattr(provider, name, None)
+        if isinstance(v, int) and not isinstance(v, bool) and v > 0:
+            return v
+    return 0
+
+
 class ProviderBatchedLM:
     """``prefill(context, B, max_new)`` / ``step(tokens)`` over a ``next_token_probs`` provider: every stream's
     context grows by its emitted token, each step queries the provider once per stream (on the host -- that is
@@ -197,7 +205,9 @@ class ProviderBatchedLM:
         self.window = int(context_window) if context_window else None
         self._first_ctx = tuple(int(t) for t in context)
         self._first = first if first is not None else provider.next_token_probs(self._trim(self._first_ctx))
-        V = dist_vocab(self._first)
+        # a dict ProbDist names only its support: the id range is the provider's declared vocabulary
+        # (MockLM.vocab_size, a model's vocab) when it has one, else what the first distribution implies
+        V = max(dist_vocab(self._first), _declared_vocab(provider))
         if V < 2:
             raise ConfigurationError("the provider's distribution needs at least two token ids")
         self.shape = SimpleNamespace(vocab=V, n_positions=0)
@@ -220,7 +230,11 @@ class ProviderBatchedLM:
                 dist = self._first
             else:
                 dist = self.provider.next_token_probs(self._trim(ctx))
-            out[b, :V] = dist_to_row(dist, V)
+            try:
+                out[b, :V] = dist_to_row(dist, V)
+            except ConfigurationError as exc:
+                raise ConfigurationError(f"{exc} (the provider declares no vocab_size; the first distribution "
+                                         f"implied {V} ids)") from None
         lg = np.zeros((len(self.ctxs), self.ld), dtype=np.float32)
         lg[:, :V] = probs_to_logits(out[:, :V])
         return torch.from_numpy(lg).to(self.device)

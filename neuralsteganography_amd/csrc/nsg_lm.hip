@@ -46,9 +46,14 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
-    // GPT-2 gelu_new: 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+    // GPT-2 gelu_new: 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3), evaluated as the equal
+    // x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 and one v_rcp_f32 (about 1 ulp each) instead of the
+    // library tanhf (a branchy polynomial / exp / IEEE-division sequence that cost as much VALU time per 128 x 128
+    // tile as the tile's MFMAs).  Relative error a few fp32 ulp before the fp16 rounding of the output; large |u|
+    // saturates cleanly (exp2 -> inf gives x * 0 = -0, exp2 -> 0 gives x).
     const float u = 0.7978845608028654f * (x + 0.044715f * (x * x * x));
-    return 0.5f * x * (1.0f + tanhf(u));
+    const float e = __builtin_amdgcn_exp2f(u * -2.8853900817779268f);  // -2 log2(e)
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 // fp32 -> fp16 with the fp32 value pinned first: without the barrier the compiler may fold the producing
@@ -386,6 +391,442 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tiled(const f16* __restrict
     }
 }
 
+// ------------------------------------------------------------------------------------------------ persistent
+// gemm_persist<NST, SPLIT, EPI>: 128 x 128 tiles, 4 waves of 64 x 64, ONE workgroup per CU looping over the tiles
+// t = g, g + G, g + 2G, ... (g = XCD-remapped id, same grouped tile order as gemm_tiled).  The LDS ring runs over
+// the concatenated K-tile sequence of all of the workgroup's tiles, so the next tile's first K-tiles are in flight
+// during this tile's last ones and its epilogue: at K = 768 a tile is only 12 K-tiles, and in the one-tile-per-
+// workgroup kernel the pipeline fill and the epilogue of every tile were exposed.
+// The waits are counted exactly: the epilogue stores go through a buffer resource whose range check drops the
+// rows >= M, so every wave issues exactly FN * FM stores per tile, none of them branched around; the bias (N <=
+// PB_BIAS_MAX) is staged in LDS once, so the epilogue issues no vector-memory load (a plain load in flight beside
+// the LDS-DMA makes the compiler drain the whole ring with vmcnt(0)).  Requires N % 128 == 0 and the output within
+// 32-bit buffer offsets (host check); every element is the same canonical MFMA chain as in gemm_tiled.
+constexpr int PB_BIAS_MAX = 4096;
+
+template <int N_>
+__device__ __forceinline__ void wait_vm_le(int n) {
+    // s_waitcnt vmcnt(k) for the largest multiple of 8 not above n (waiting for MORE is always safe)
+    if constexpr (N_ > 0) {
+        if (n >= N_) {
+            wait_vm<N_>();
+            return;
+        }
+        wait_vm_le<N_ - 8>(n);
+    } else {
+        wait_vm<0>();
+    }
+}
+
+template <int NST, bool SPLIT, int EPI>
+__global__ __launch_bounds__(256) void gemm_persist(const f16* __restrict__ X, int64_t ldx,
+                                                    const f16* __restrict__ Wt, int64_t ldw,
+                                                    const f16* __restrict__ bias, void* Y, int64_t ldy, int M, int N,
+                                                    int K) {
+    constexpr int BN = 128, BM = 128, WM = 2, NT = 256, NW = 4, FN = 4, FM = 4;
+    constexpr int ROWS = BN + BM, GL = ROWS * 8 / NT, SB = ROWS * 128;
+    constexpr int NSTO = FN * FM;  // epilogue stores per wave and tile
+    constexpr int ESZ = EPI == NS_LM_EPI_STORE_F32 ? 4 : 2;
+    static_assert(NST >= 2 && NST <= 4 && GL == 8, "ring");
+    __shared__ __attribute__((aligned(16))) char smem[NST * SB + PB_BIAS_MAX * 2];
+    f16* s_bias = (f16*)(smem + NST * SB);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wn = wave / WM, wm = wave - wn * WM;
+    const int fr = lane & 15, fc = lane >> 4;
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN, T = tiles_m * tiles_n;
+    const int G = gridDim.x, g = xcd_remap(blockIdx.x, G);
+    const int KT = K / BK, SK = k_chains(K), TPC = (KT + SK - 1) / SK;
+    const int ntl = g < T ? (T - 1 - g) / G + 1 : 0;
+    const int S = ntl * KT;  // K-tiles this workgroup runs, all tiles concatenated
+
+    if (bias) {
+        for (int i = threadIdx.x * 8; i < N; i += NT * 8) *(f16x8*)(s_bias + i) = *(const f16x8*)(bias + i);
+    }
+    __syncthreads();  // no LDS-DMA in flight yet
+
+    auto origin = [&](int i, int& n0, int& m0) {
+        constexpr int GN = 1024 / BN;
+        const int t = g + i * G;
+        const int grp = t / (GN * tiles_m), within = t - grp * (GN * tiles_m);
+        const int gn = min(GN, tiles_n - grp * GN);
+        const int tm = within / gn;
+        n0 = (grp * GN + (within - tm * gn)) * BN;
+        m0 = tm * BM;
+    };
+    // staging: instruction q of the wave fills LDS rows (q * NW + wave) * 8 .. +7; q < GL/2 are weight rows
+    const int srow = lane >> 3;
+    auto stage = [&](int i, int kt, int buf) {
+        int n0, m0;
+        origin(i, n0, m0);
+        char* dst = smem + buf * SB;
+#pragma unroll
+        for (int q = 0; q < GL; ++q) {
+            const int qq = q * NW + wave;
+            const int row = qq * 8 + srow;
+            const int chunk = (lane & 7) ^ swz(row);
+            const f16* src = q < GL / 2 ? Wt + (int64_t)(n0 + row) * ldw
+                                        : X + (int64_t)min(m0 + row - BN, M - 1) * ldx;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + chunk * 8 + kt * BK),
+                                             (__attribute__((address_space(3))) void*)(dst + qq * 8 * 128), 16, 0, 0);
+        }
+    };
+
+    // output resource: offsets past M rows fail the range check and the store is dropped
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(Y, (short)0, (int)((int64_t)M * ldy * ESZ), 0x00020000);
+
+    f32x4 acc[FN][FM];
+    f32x4 tot[SPLIT ? FN : 1][SPLIT ? FM : 1];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int is_i = 0, is_k = 0, is_n = 0;  // next stage to issue: tile, K-tile, sequence number
+    auto issue = [&]() {
+        stage(is_i, is_k, is_n % NST);
+        ++is_n;
+        if (++is_k == KT) {
+            is_k = 0;
+            ++is_i;
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < NST - 1; ++p)
+        if (is_n < S) issue();
+
+    int ci = 0, ck = 0;
+    unsigned epmask = 0;  // bit d: the iteration d + 1 back ran an epilogue
+    for (int s = 0; s < S; ++s) {
+        // younger than stage s's copies: stages s+1 .. s+NST-2 and the stores of epilogues since its issue
+        const int ahead = min(NST - 2, S - 1 - s);
+        const int nep = __builtin_popcount(epmask & ((1u << (NST - 1)) - 1u));
+        wait_vm_le<56>(GL * ahead + NSTO * nep);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (is_n < S) issue();  // into the buffer read one iteration ago (every wave is past this barrier)
+        if constexpr (SPLIT) {
+            if (ck > 0 && ck % TPC == 0) {
+#pragma unroll
+                for (int i = 0; i < FN; ++i)
+#pragma unroll
+                    for (int j = 0; j < FM; ++j) {
+                        tot[i][j] = ck == TPC ? acc[i][j] : tot[i][j] + acc[i][j];
+                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+            }
+        }
+        const char* base = smem + (s % NST) * SB;
+        f16x8 a[2][FN], b[2][FM];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + fc;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int row = wn * FN * 16 + i * 16 + fr;
+                a[kk][i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int row = BN + wm * FM * 16 + j * 16 + fr;
+                b[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[kk][i], b[kk][j], acc[i][j]);
+        epmask <<= 1;
+        if (ck == KT - 1) {
+            if constexpr (SPLIT) {
+                if (KT > TPC) {
+#pragma unroll
+                    for (int i = 0; i < FN; ++i)
+#pragma unroll
+                        for (int j = 0; j < FM; ++j) acc[i][j] = tot[i][j] + acc[i][j];
+                }
+            }
+            int n0, m0;
+            origin(ci, n0, m0);
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int n = n0 + wn * FN * 16 + i * 16 + 4 * fc;
+                f16x4 bb = f16x4{};
+                if (bias) bb = *(const f16x4*)(s_bias + n);
+#pragma unroll
+                for (int j = 0; j < FM; ++j) {
+                    const int m = m0 + wm * FM * 16 + j * 16 + fr;
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = bias ? acc[i][j][r] + (float)bb[r] : acc[i][j][r];
+                    const int off = (int)(((int64_t)m * ldy + n) * ESZ);
+                    if constexpr (EPI == NS_LM_EPI_STORE_F32) {
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                         __float_as_uint(v[3])};
+                        __builtin_amdgcn_raw_buffer_store_b128(w, rs, off, 0, 0);
+                    } else {
+                        f16x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = EPI == NS_LM_EPI_GELU ? to_f16(gelu_tanh(v[r])) : to_f16(v[r]);
+                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rs, off, 0, 0);
+                    }
+                    acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            epmask |= 1u;
+            ck = 0;
+            ++ci;
+        } else {
+            ++ck;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------------- big
+// gemm_big<EPI>: 256 x 256 tiles, 8 waves (4 along N x 2 along M) of 64 x 128, K <= 1024 (one K chain), one
+// workgroup per CU (two 64 KiB LDS buffers).  Why this shape: per K-tile a wave issues 8 LDS-DMA pieces
+// whatever the tile, but a 64 x 128 wave tile gives it 64 MFMAs to hide them behind (a 128 x 128 tile's 64 x 64
+// wave tiles: 32), and the operand bytes per MFMA out of LDS halve.  One barrier per K-tile: tile kt + 1's
+// copies are issued in the first half of tile kt's MFMAs (into the buffer every wave finished reading before the
+// previous barrier) and waited for at its end.  Ragged N and M: rows clamped on load, columns / rows >= N / M
+// not stored.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_big(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
+                                                int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
+                                                int M, int N, int K) {
+    constexpr int BN = 256, BM = 256, NW = 8, WM = 2, FN = 4, FM = 8, FH = FM / 2;
+    constexpr int ROWS = BN + BM, GL = ROWS * 8 / (64 * NW), SB = ROWS * 128;
+    static_assert(GL == 8, "staging");
+    __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    constexpr int GN = 4;  // weight panels per group (1024 rows)
+    const int grp = t / (GN * tiles_m), within = t - grp * (GN * tiles_m);
+    const int gn = min(GN, tiles_n - grp * GN);
+    const int tm = within / gn, tn = grp * GN + (within - tm * gn);
+    const int n0 = tn * BN, m0 = tm * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wn = wave / WM, wm = wave - wn * WM;
+    const int fr = lane & 15, fc = lane >> 4;
+
+    const f16* src[GL];
+    int lds_off[GL];
+#pragma unroll
+    for (int q = 0; q < GL; ++q) {
+        const int qq = q * NW + wave;
+        const int row = qq * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ swz(row);
+        src[q] = (q < GL / 2 ? Wt + (int64_t)min(n0 + row, N - 1) * ldw
+                             : X + (int64_t)min(m0 + row - BN, M - 1) * ldx) + chunk * 8;
+        lds_off[q] = qq * 8 * 128;
+    }
+    auto piece = [&](int q, int kt, int buf) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[q] + kt * BK),
+                                         (__attribute__((address_space(3))) void*)(smem + buf * SB + lds_off[q]), 16,
+                                         0, 0);
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int KT = K / BK;
+#pragma unroll
+    for (int q = 0; q < GL; ++q) piece(q, 0, 0);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int kt = 0; kt < KT; ++kt) {
+        const int buf = kt & 1;
+        const bool nxt = kt + 1 < KT;
+        const char* base = smem + buf * SB;
+        f16x8 a[2][FN], b0[2][FH], b1[2][FH];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + fc;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int row = wn * FN * 16 + i * 16 + fr;
+                a[kk][i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < FH; ++j) {
+                const int row = BN + wm * FM * 16 + j * 16 + fr;
+                b0[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+        }
+        if (nxt) {
+#pragma unroll
+            for (int q = 0; q < GL; ++q) piece(q, kt + 1, buf ^ 1);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + fc;
+#pragma unroll
+            for (int j = 0; j < FH; ++j) {
+                const int row = BN + wm * FM * 16 + (FH + j) * 16 + fr;
+                b1[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FH; ++j) acc[i][j] = mfma16(a[kk][i], b0[kk][j], acc[i][j]);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FH; ++j) acc[i][FH + j] = mfma16(a[kk][i], b1[kk][j], acc[i][FH + j]);
+        if (nxt) wait_vm<0>();
+        lds_fence_barrier();  // tile kt + 1 landed everywhere; every wave is done reading buffer kt & 1
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * FN * 16 + i * 16 + 4 * fc;
+        if (n >= N) continue;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int m = m0 + wm * FM * 16 + j * 16 + fr;
+            if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[i][j]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ ping-pong
+// gemm_pp<EPI>: the 256 x 256 tile of gemm_big with its two wave groups (g = 0: activation rows 0..127 of the
+// tile, g = 1: rows 128..255; each 4 waves of 64 weight rows x 128 rows) run half a K-tile apart, so that on every
+// SIMD (one wave of each group) one wave issues MFMAs while the other reads its next fragments and stages the
+// next K-tile (ping-pong; the MFMA wave runs at raised priority).  Time is cut into slots by workgroup barriers;
+// group 0 runs L(t) (LDS reads of K-tile t, staging of t + 1) in slot 2t+1 and M(t) (64 MFMAs) in slot 2t+2,
+// group 1 one slot later (one extra barrier up front, group 0 one extra at the end).  Staging: group 0 copies the
+// weight panel and its activation rows (12 pieces per wave), group 1 its activation rows (4 pieces).  Hazards,
+// by slot: a wave ends every L slot with lgkmcnt(0) (its reads of buffer t & 1 are complete at that barrier) and
+// every M slot with vmcnt(0) (its copies of t + 1 have landed): K-tile t+1 goes into the buffer last read in slot
+// 2t (group 1's L(t-1)), and is read from slot 2t+3 (group 0) / 2t+4 (group 1) on, after the barriers that follow
+// its writers' waits.  One K chain (K <= 1024); ragged N / M clamped on load, not stored.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_pp(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
+                                               int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
+                                               int N, int K) {
+    constexpr int BN = 256, BM = 256, FN = 4, FM = 8, SB = (BN + BM) * 128;
+    __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    constexpr int GN = 4;
+    const int grp = t / (GN * tiles_m), within = t - grp * (GN * tiles_m);
+    const int gn = min(GN, tiles_n - grp * GN);
+    const int tm = within / gn, tn = grp * GN + (within - tm * gn);
+    const int n0 = tn * BN, m0 = tm * BM;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = wave >> 2, wn = wave & 3;
+    const int fr = lane & 15, fc = lane >> 4;
+    const int lr = lane >> 3;
+    // piece q of a wave covers LDS rows qq * 8 + lr; (qq * 8 >> 1) & 7 == (wn * 4) & 7 for every q, so the swizzle
+    // chunk is the same for all of a wave's pieces
+    const int chunk = (lane & 7) ^ ((wn * 4 + (lane >> 4)) & 7);
+    auto stage = [&](int kt, int buf) {
+        char* dst = smem + buf * SB;
+        // the twelve row pointers are recomputed per call (an opaque copy of the lane's row keeps the compiler from
+        // hoisting them out of the K loop: 24 live VGPRs would spill next to the 96 fragment and 128 accumulator
+        // registers)
+        int r8 = wn * 8 + lr;
+        asm volatile("" : "+v"(r8));
+        if (g == 0) {
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                const f16* p = q < 8 ? Wt + (int64_t)min(n0 + q * 32 + r8, N - 1) * ldw
+                                     : X + (int64_t)min(m0 + (q - 8) * 32 + r8, M - 1) * ldx;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + chunk * 8 + kt * BK),
+                                                 (__attribute__((address_space(3))) void*)(dst + (q * 4 + wn) * 1024),
+                                                 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f16* p = X + (int64_t)min(m0 + 128 + q * 32 + r8, M - 1) * ldx;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + chunk * 8 + kt * BK),
+                                                 (__attribute__((address_space(3))) void*)(dst + (48 + q * 4 + wn) * 1024),
+                                                 16, 0, 0);
+            }
+        }
+    };
+    auto barrier = []() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int KT = K / BK;
+    stage(0, 0);
+    wait_vm<0>();
+    barrier();
+    if (g == 1) barrier();  // group 1 starts one slot late
+    for (int kt = 0; kt < KT; ++kt) {
+        const int buf = kt & 1;
+        const char* base = smem + buf * SB;
+        // ---- L slot: this K-tile's fragments, the next K-tile's copies
+        f16x8 a[2][FN], b[2][FM];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + fc;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int row = wn * FN * 16 + i * 16 + fr;
+                a[kk][i] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int row = BN + g * FM * 16 + j * 16 + fr;
+                b[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+            }
+        }
+        if (kt + 1 < KT) stage(kt + 1, buf ^ 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+        // ---- M slot
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = mfma16(a[kk][i], b[kk][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (kt + 1 < KT) wait_vm<0>();
+        barrier();
+    }
+    if (g == 0) barrier();  // same barrier count for both groups
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * FN * 16 + i * 16 + 4 * fc;
+        if (n >= N) continue;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int m = m0 + g * FM * 16 + j * 16 + fr;
+            if (m < M) store4<EPI>(Y, ldy, bias, m, n, acc[i][j]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ layernorm
 constexpr int LN_MAXV = 8;  // f16x4 vectors per lane: C <= 2048
 
@@ -509,8 +950,31 @@ enum GemmCfg {
     CFG_T128x256_2,                                   // 128 x 256, 8 waves
     CFG_T64_4,                                        // 64 x 64, 4 stages
     CFG_T128x64_3,                                    // 128 weight rows x 64 activation rows, 4 waves, 3 stages
+    CFG_B256,                                         // 256 x 256, 8 waves of 64 x 128 (K <= 1024)
+    CFG_P128_2, CFG_P128_3, CFG_P128_4,               // persistent 128 x 128, 2 / 3 / 4 stages (2 / 1 / 1 per CU)
+    CFG_PP256,                                        // 256 x 256, two ping-pong wave groups (K <= 1024)
     CFG_COUNT
 };
+
+static int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
+}
+
+// gemm_persist's preconditions (else the persistent configurations run the 128 x 128 tiled kernel: same bits)
+static bool persist_ok(int epi, const void* bias, int64_t ldy, int M, int N) {
+    const int64_t esz = epi == NS_LM_EPI_STORE_F32 ? 4 : 2;
+    return epi != NS_LM_EPI_RESIDUAL && N % 128 == 0 && (!bias || N <= PB_BIAS_MAX) &&
+           ((int64_t)M + 128) * ldy * esz < ((int64_t)1 << 31);
+}
 
 template <int FM, int EPI>
 static void launch_direct(const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y,
@@ -559,6 +1023,50 @@ static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_
         case CFG_T128x256_2: NSG_TILED(128, 256, 2, 4, 2); break;
         case CFG_T64_4: NSG_TILED(64, 64, 2, 2, 4); break;
         case CFG_T128x64_3: NSG_TILED(128, 64, 2, 2, 3); break;
+        case CFG_B256:
+            if (split) {  // one K chain only (K <= 1024); else the 128 x 128 tiles (same bits)
+                NSG_TILED(128, 128, 2, 2, 2);
+            } else {
+                hipLaunchKernelGGL((gemm_big<EPI>), tiles(256, 256), dim3(512), 0, st, x, ldx, wt, ldw, bias, y, ldy,
+                                   M, N, K);
+            }
+            break;
+        case CFG_PP256:
+            if (split) {
+                NSG_TILED(128, 128, 2, 2, 2);
+            } else {
+                hipLaunchKernelGGL((gemm_pp<EPI>), tiles(256, 256), dim3(512), 0, st, x, ldx, wt, ldw, bias, y, ldy, M,
+                                   N, K);
+            }
+            break;
+        case CFG_P128_2:
+        case CFG_P128_3:
+        case CFG_P128_4: {
+            if (!persist_ok(EPI, bias, ldy, M, N)) {
+                NSG_TILED(128, 128, 2, 2, 2);
+                break;
+            }
+            const int T = ((M + 127) / 128) * (N / 128);
+            const int G = min(T, cu_count() * (cfg == CFG_P128_2 ? 2 : 1));
+            if constexpr (EPI != NS_LM_EPI_RESIDUAL) {
+#define NSG_PERSIST(NSTv)                                                                                        \
+    if (split)                                                                                                   \
+        hipLaunchKernelGGL((gemm_persist<NSTv, true, EPI>), dim3(G), dim3(256), 0, st, x, ldx, wt, ldw, bias, y, \
+                           ldy, M, N, K);                                                                        \
+    else                                                                                                         \
+        hipLaunchKernelGGL((gemm_persist<NSTv, false, EPI>), dim3(G), dim3(256), 0, st, x, ldx, wt, ldw, bias, y, \
+                           ldy, M, N, K)
+                if (cfg == CFG_P128_2) {
+                    NSG_PERSIST(2);
+                } else if (cfg == CFG_P128_3) {
+                    NSG_PERSIST(3);
+                } else {
+                    NSG_PERSIST(4);
+                }
+#undef NSG_PERSIST
+            }
+            break;
+        }
 #undef NSG_DIRECT
 #undef NSG_TILED
         default: break;
@@ -574,6 +1082,9 @@ static int auto_cfg(int M, int N, int K) {
     if (M <= 16) return (N >= 8192 && !split) ? CFG_T64_2 : CFG_DIRECT16;
     if (split && M <= 256) return M <= 64 ? CFG_DIRECT16 : M <= 128 ? CFG_DIRECT32 : CFG_DIRECT64;
     if (N >= 8192 && M >= 512) return CFG_T128_2;
+    // GPT-2's c_fc at B >= 4096 (profiles/lmprobe_r03o_b4096.jsonl: 581 vs 501 TFLOP/s for the 64 x 64 tiles);
+    // c_attn (N = 2304) and the smaller batches stay on the 64 x 64 tiles (more tiles than CUs)
+    if (!split && M >= 4096 && N >= 2560) return CFG_PP256;
     return CFG_T64_2;
 }
 

@@ -140,12 +140,13 @@ class BatchedGPT2:
             want = min(int(want), int(self.position_cap))
         if self.device.type != "cuda":
             return int(want)
+        # the previous cache is dropped first and the caching allocator's idle segments returned to the device:
+        # counting them as free instead is wrong once a small tensor has been carved out of a freed cache block
+        # (the segment cannot be released then, and a cache of a slightly larger size does not fit the hole;
+        # seen as a 120 GiB OOM between two encodes of different batch sizes)
+        self.k_cache = self.v_cache = None
+        torch.cuda.empty_cache()
         free, _ = torch.cuda.mem_get_info(self.device)
-        # memory PyTorch's caching allocator holds but no tensor uses (e.g. a previous call's KV cache) is free too
-        # (the allocator releases cached blocks and retries when a request does not fit one of them)
-        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-        if self.k_cache is not None:
-            free += 2 * self.k_cache.numel() * self.k_cache.element_size()
         return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
 
     def _native_buffers(self, B: int):

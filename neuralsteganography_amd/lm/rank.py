@@ -67,7 +67,11 @@ class HipRankLM:
             batched_lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
         self.lm = batched_lm
         self.vocab = self.lm.shape.vocab
-        self.tokenizer = tokenizer if tokenizer is not None else ByteTokenizer(self.vocab)
+        # the byte stand-in only where it can spell bytes (a small provider vocabulary has no tokenizer: its
+        # callers pass token ids, and encode_seed then raises)
+        if tokenizer is None and self.vocab >= 257:
+            tokenizer = ByteTokenizer(self.vocab)
+        self.tokenizer = tokenizer
         self.logits_dtype = logits_dtype
         self.max_batch = int(max_batch)
         self.device_index = torch.cuda.current_device()
@@ -92,6 +96,8 @@ class HipRankLM:
     # ------------------------------------------------------------------ protocol (api.py:42-56)
     def encode_seed(self, text: str) -> List[int]:
         tok = self.tokenizer
+        if tok is None:
+            raise ConfigurationError(f"no tokenizer for a {self.vocab}-id vocabulary: pass token ids as context")
         try:
             bos = list(tok.encode("<|endoftext|>", add_special_tokens=False))
         except TypeError:

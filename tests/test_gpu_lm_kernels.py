@@ -139,6 +139,37 @@ def test_gemm_tile_configurations_agree_bitwise(M, N, K, epi):
                                         None) == _lib.NS_ERR_CONFIG
 
 
+@pytest.mark.parametrize("M,N,K,epi,with_bias", [(1100, 8192, 768, "f32", False), (4096, 3072, 768, "gelu", True),
+                                                  (777, 2304, 768, "store", True), (300, 1024, 3072, "gelu", True),
+                                                  (129, 1536, 2048, "f32", True), (5000, 768, 64, "store", False),
+                                                  (333, 2176, 768, "f32", False)])
+def test_gemm_persistent_configurations_agree_bitwise(M, N, K, epi, with_bias):
+    """The 256 x 256 (plain and ping-pong) and persistent 128 x 128 kernels (one workgroup per CU looping over
+    several tiles): ragged last row / column blocks, K-chain splits, one-K-tile tiles, with and without bias) give the tiled kernel's bits and the fp64 result."""
+    x, wt, bias = _operands(M, N, K, seed=M + 3 * N + K)
+    b = bias if with_bias else None
+    ydt = torch.float32 if epi == "f32" else torch.float16
+    y0 = torch.full((M + 1, N), 7.0, device="cuda").to(ydt)  # one guard row past M: never written
+    L = _lib.lib()
+    n = L.ns_lm_gemm_configs()
+
+    def run(cfg):
+        y = y0.clone()
+        rc = L.ns_lm_gemm_config(x.data_ptr(), K, wt.data_ptr(), K, b.data_ptr() if b is not None else None,
+                                 y.data_ptr(), N, M, N, K, EPIS[epi], cfg, _stream_handle())
+        assert rc == 0
+        torch.cuda.synchronize()
+        return y
+
+    ref = run(6)  # CFG_T128_3
+    assert torch.equal(ref[M], y0[M])
+    want = _ref(x, wt, b, None, epi)
+    assert ((ref[:M].double() - want).abs() <= 2e-3 * want.abs() + 2e-3).all()
+    for cfg in range(13, n):  # from CFG_B256 on: the 256 x 256, persistent and ping-pong kernels
+        y = run(cfg)
+        assert torch.equal(y, ref), cfg
+
+
 @pytest.mark.parametrize("M,C", [(1, 768), (7, 1024), (300, 768), (5, 64), (33, 1600)])
 def test_layernorm_matches_torch(M, C):
     g = torch.Generator(device="cuda").manual_seed(M + C)

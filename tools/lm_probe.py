@@ -58,10 +58,12 @@ def main():
     shapes = [("c_attn", lw["qkv_wt"], lw["qkv_b"], lw["qkv_w"], C, 0), ("attn_proj", lw["o_wt"], lw["o_b"], lw["o_w"], C, 2),
               ("c_fc", lw["fc_wt"], lw["fc_b"], lw["fc_w"], C, 1), ("mlp_proj", lw["pr_wt"], lw["pr_b"], lw["pr_w"], 4 * C, 2),
               ("lm_head", lm.head_t, None, lm.head, C, 0)]
+    # the same shapes with a plain store (the epilogue's own cost) and the fp32-logits head the bench's coder reads
+    shapes += [("c_fc_store", lw["fc_wt"], lw["fc_b"], lw["fc_w"], C, 0), ("lm_head_f32", lm.head_t, None, lm.head, C, 3)]
     for name, wt, bias, w, K, epi in ([] if args.attn_only else shapes):
         N = wt.shape[0]
         xa = x[:, :K].contiguous()
-        y = torch.empty((B, N), device=dev).half()
+        y = torch.empty((B, N), device=dev, dtype=torch.float32 if epi == 3 else torch.float16)
         st = _stream_handle()
         bp = bias.data_ptr() if bias is not None else None
 
