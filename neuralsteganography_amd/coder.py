@@ -87,6 +87,25 @@ class CoderParams:
             raise ConfigurationError(f"at most {_lib.NS_MAX_BANNED} banned ids")
 
 
+_DEFERRED: List[tuple] = []  # (device, handle) of contexts closed during a graph capture
+
+
+def _destroy(device: int, h) -> None:
+    torch = _torch()
+    if torch.cuda.is_available():  # launches still queued may read the context's buffers
+        torch.cuda.synchronize(device)
+    _lib.lib().ns_destroy(h)
+
+
+def _drain_deferred() -> None:
+    torch = _torch()
+    if not _DEFERRED or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        return
+    while _DEFERRED:
+        dev, h = _DEFERRED.pop()
+        _destroy(dev, h)
+
+
 class CoderContext:
     """Owns an ``ns_ctx`` (device, vocab, precision, dtype, max batch)."""
 
@@ -95,6 +114,7 @@ class CoderContext:
         torch = _torch()
         if not torch.cuda.is_available():
             raise _lib.NativeLibraryError("the HIP coder needs a ROCm GPU (torch.cuda.is_available() is False)")
+        _drain_deferred()
         self.params = params
         self.device = torch.cuda.current_device() if device is None else int(device)
         self.max_batch = int(max_batch)
@@ -136,12 +156,20 @@ class CoderContext:
         return [int(v) for v in out]
 
     def close(self) -> None:
-        if getattr(self, "_h", None):
-            torch = _torch()
-            if torch.cuda.is_available():  # launches still queued may read the context's buffers
-                torch.cuda.synchronize(self.device)
-            _lib.lib().ns_destroy(self._h)
-            self._h = None
+        """Release the context.  Launches still queued may read its buffers, so the device is synchronised
+        first -- except while the current stream is capturing a hipGraph (a garbage-collected context during
+        a capture): a device-wide sync or a free there would invalidate the capture, so the handle is parked
+        and destroyed by the next close() or context creation outside a capture."""
+        h = getattr(self, "_h", None)
+        if not h:
+            return
+        self._h = None
+        torch = _torch()
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            _DEFERRED.append((self.device, h))
+            return
+        _destroy(self.device, h)
+        _drain_deferred()
 
     def __del__(self):  # pragma: no cover - interpreter shutdown order
         try:

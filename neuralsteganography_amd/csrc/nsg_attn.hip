@@ -160,7 +160,16 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     typedef typename F::Raw Raw;
     constexpr int DPL = F::DPL, LPR = F::LPR, RPI = F::RPI, NI = F::NI;
     if (L0p) L0 = __builtin_amdgcn_readfirstlane(*L0p);  // graph replays: the cache length lives on the device
-    if (L0 < T0 || L0 >= cap) return;                    // never write past the cache (host checks capacity)
+    if (L0 < T0 || L0 >= cap) {  // never write past the cache (the host checks capacity); with a device-side L0
+        // the host cannot see an overflow before the launch, so poison this workgroup's output rows: the NaNs
+        // reach the logits and the coder rejects them, instead of the next GEMM reusing stale rows
+        for (int i = threadIdx.x; i < P * ATT_D; i += blockDim.x) {
+            const int pair = blockIdx.x * P + i / ATT_D;
+            if (pair < B * H)
+                out[(int64_t)(pair / H) * out_stride + (pair % H) * ATT_D + i % ATT_D] = (_Float16)__builtin_nanf("");
+        }
+        return;
+    }
     __shared__ float s_m[8], s_l[8];
     __shared__ float s_acc[8][ATT_D];
     const int Lk = L0 + 1;

@@ -952,6 +952,13 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     to_keys(cand, lane);
     NSG_STAMP(p, b, lane, 4);
     if (cand.cnt > K) compact_topk(keys, cand.scr, cand.cnt, K, lane);
+    // fewer than K candidates after the exact re-stream: the row holds NaN logits (never candidates; every
+    // other valid id passes a -inf threshold).  Zero the missing keys (no stale LDS) and report a range error.
+    const bool short_row = cand.cnt < K;
+    if (short_row) {
+        for (int i = cand.cnt + lane; i < K; i += WAVE) keys[i] = 0ull;
+        lds_fence();
+    }
     NSG_STAMP(p, b, lane, 5);
     const int nsk = (K + WAVE - 1) / WAVE;
     const int K8 = (K + 7) & ~7;
@@ -1159,6 +1166,10 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
                 if (lane == 0 && kp < p.ranked_stride) rk_out[kp] = -1;
             }
         }
+    }
+    if (short_row || !(E > 0.0 && E <= 1.7976931348623157e308)) {  // NaN / +inf logits (e.g. a poisoned
+        sel = -1;  // attention row): the CDF is meaningless, report a range error, emit nothing
+        err = NS_ST_ERR_RANGE;
     }
 
     uint64_t tk = 0;

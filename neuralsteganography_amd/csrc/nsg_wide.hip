@@ -450,6 +450,11 @@ __device__ __forceinline__ void wide_cdf_stream(const StepParams& p, const WideS
     const ns_stream_state st = p.state[b];
     const uint64_t* sk = keys_sorted + (int64_t)b * cap;
     const int nC = (int)count[b];
+    if (nC < 2) {  // every row has >= 2 valid ids and the collection keeps the top two: only NaN logits (never
+        // collected) get here -- no CDF exists, report a range error instead of reading stale keys
+        if (tid == 0) p.state[b].flags = st.flags | NS_ST_ERR_RANGE | NS_ST_DONE;
+        return;
+    }
     const int Kc = min(nC, p.K);
     const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
     const double m = (double)wkey_val(sk[0]);
@@ -661,6 +666,7 @@ __device__ __forceinline__ void wide_cdf_stream(const StepParams& p, const WideS
     }
     const int sel = block_min_int(sel_l, smi);
     if (sel == 0x7FFFFFFF) err = DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE;
+    if (!(E > 0.0 && E <= 1.7976931348623157e308)) err = NS_ST_ERR_RANGE;  // non-finite logits: no valid CDF
     if (DECODE && err && p.ranked) {  // ranked kept ids for the host's BPE repair (arithmetic.py:300-342)
         int32_t* rk_out = p.ranked + (int64_t)b * p.ranked_stride;
         for (int i = tid; i < kp && i < p.ranked_stride; i += WIDE_THREADS) rk_out[i] = (int32_t)wkey_id(sk[i]);
@@ -915,6 +921,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         }
     }
     // ---- sorted keys of this thread's ranks into registers; s_keys becomes the e_i array
+    NSG_STAMP(p, b, tid, 5);
     uint64_t ks[FAST_R];
 #pragma unroll
     for (int r = 0; r < FAST_R; ++r) {
@@ -1007,6 +1014,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         for (int i = 0; i < FAST_WAVES; ++i) fb = min(fb, s_i[i]);
         fa = Kc;
     }
+    NSG_STAMP(p, b, tid, 6);
 #if NSG_SCAN_DIAG == 4  // timing diagnostics: up to the cutoff
     if (tid == 0) atomicExch((unsigned int*)&keys_out[(int64_t)b * cap], (unsigned int)(fb + fa));
     return;
@@ -1099,6 +1107,7 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     publish(kp - 1, 0, false);
     __syncthreads();
     const int64_t cum_kp = s_c[0];
+    NSG_STAMP(p, b, tid, 7);
     const int64_t shift = (int64_t)R - cum_kp + (int64_t)st.lo;
     // ---- selection
     int sel = 0x7FFFFFFF;
@@ -1127,7 +1136,8 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < FAST_WAVES; ++i) sel = min(sel, s_k[i]);
-    if (sel == 0x7FFFFFFF) {  // range / divergence error: wide_cdf_kernel reports it (and the ranked export)
+    if (sel == 0x7FFFFFFF || !(E > 0.0 && E <= 1.7976931348623157e308)) {  // range / divergence error or
+        // non-finite logits: wide_cdf_kernel reports it (and the ranked export)
         defer();
         return;
     }
@@ -1160,6 +1170,8 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
     }
     wide_finish<DECODE>(p, b, st, k, kp, sel, exact, S_used, s_c[1], s_c[2], shift, (uint64_t)s_c[3], m, rs, kl,
                         want_stats);
+    NSG_STAMP(p, b, tid, 8);
+    NSG_STAMP_RT(p, b, tid, 10);
 }
 
 
@@ -1540,6 +1552,8 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
     const int ntiles = (V + TS - 1) / TS;
     const int per = (ntiles + FAST_WAVES - 1) / FAST_WAVES;
+    NSG_STAMP_RT(p, b, tid, 9);
+    NSG_STAMP(p, b, tid, 0);
     const int s0 = min(ntiles, wv * per), s1 = min(ntiles, s0 + per);
     const int ns = min(NSW, s1 - s0);  // sample tiles: the last ns tiles of the slice
     const int se = s1 - ns;            // streamed tiles [s0, se)
@@ -1729,6 +1743,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
 #pragma unroll
     for (int i = 0; i < NSW; ++i)
         if (i < ns) append_tile(se + i, xs[i], mbs[i]);
+    NSG_STAMP(p, b, tid, 1);
 
     // ---- stream the rest of the slice; the threshold rises every UPD tiles (16 values per lane)
     constexpr int UPD = 16 / W;
@@ -1767,6 +1782,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     if (tid == 0) count[b] = 0u;
     return;
 #endif
+    NSG_STAMP(p, b, tid, 2);
 
     // ---- the row's statistics
     accS = wave_sum_butterfly(accS);
@@ -1833,6 +1849,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     }
     if (tid == 0) ws[b] = w;
     __syncthreads();
+    NSG_STAMP(p, b, tid, 3);
     // the row's second largest valid value (a block rescan of the row; block-uniform result)
     auto top2_second = [&]() __attribute__((always_inline)) -> float {
         float l1 = -__builtin_inff(), l2 = -__builtin_inff();
@@ -1945,6 +1962,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     }
     if (tid == 0) count[b] = (unsigned int)n;
     static_assert(FAST_R * WAVE == OP_CAPW, "one slot per buffer entry");
+    NSG_STAMP(p, b, tid, 4);
     const int mine = cnt;
     auto at = [&](int rr, uint64_t& key) __attribute__((always_inline)) -> bool {
         if (from_lds) {  // block-uniform

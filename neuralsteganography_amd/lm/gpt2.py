@@ -140,13 +140,15 @@ class BatchedGPT2:
             want = min(int(want), int(self.position_cap))
         if self.device.type != "cuda":
             return int(want)
-        # the previous cache is dropped first and the caching allocator's idle segments returned to the device:
-        # counting them as free instead is wrong once a small tensor has been carved out of a freed cache block
-        # (the segment cannot be released then, and a cache of a slightly larger size does not fit the hole;
-        # seen as a 120 GiB OOM between two encodes of different batch sizes)
+        # the previous cache is dropped first; memory PyTorch's caching allocator holds but no tensor uses (e.g.
+        # that cache, or the pre-touched one bench.py hands back) counts as free: reusing those segments keeps
+        # the pages warm (releasing them and allocating afresh measured a much slower first pass over the new
+        # cache).  When a small tensor carved out of a freed block makes the request not fit the hole (seen as a
+        # 120 GiB OOM between two encodes of different batch sizes), allocate() releases the idle segments and
+        # retries.
         self.k_cache = self.v_cache = None
-        torch.cuda.empty_cache()
         free, _ = torch.cuda.mem_get_info(self.device)
+        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
 
     def _native_buffers(self, B: int):
@@ -186,8 +188,14 @@ class BatchedGPT2:
         shp = self._cache_shape(B, max_len - T0, plain)
         # uninitialised: attention only ever reads positions < L + 1, all written before they are read
         kdt = self.kv_torch_dtype if dtype is None else dtype
-        self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
-        self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
+        try:
+            self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
+            self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
+        except torch.OutOfMemoryError:  # idle cached segments too fragmented for the request: release, retry once
+            self.k_cache = self.v_cache = None
+            torch.cuda.empty_cache()
+            self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
+            self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
         self.B, self.L, self.max_len, self.T0 = B, 0, max_len, T0
         if T0 == 0:
             self.kp = self.vp = None

@@ -216,6 +216,33 @@ def test_decode_divergence_is_reported():
         decode_batch(ctx, [[628, 1, 2], [V - 1]], fn)  # banned ids can never be decoded
 
 
+@pytest.mark.parametrize("topk", [300, 50000])  # single-pass kernel, wide path
+@pytest.mark.parametrize("poison", ["nan", "inf"])
+def test_non_finite_logits_are_reported(topk, poison):
+    """A NaN row (what the attention kernel writes when a device-side cache length is out of range) or a +inf
+    logit must surface as a range error, never as a token from a meaningless CDF."""
+    from neuralsteganography_amd.codec.errors import ArithmeticRangeError
+    from neuralsteganography_amd.coder import CoderParams, encode_batch, row_stride
+
+    torch = _torch()
+    V = 50257
+    params = CoderParams(vocab=V, precision=16 if topk > 1000 else 26, temp=1.0, topk=topk)
+    ctx = _ctx(params, 2)
+    good = _logits_fn(3, [0, 1], V, 3.0, "f32", row_stride(V, "f32"))
+
+    def fn(t, _last=None):
+        x = good(t)
+        if poison == "nan":
+            x[1].fill_(float("nan"))
+        else:
+            x[1, 17] = float("inf")
+        return x
+
+    with pytest.raises(ArithmeticRangeError):
+        encode_batch(ctx, [[1, 0, 1, 1] * 8, [0, 1, 1, 0] * 8], fn)
+    torch.cuda.synchronize()
+
+
 def test_empty_and_single_bit_payloads():
     from neuralsteganography_amd.coder import CoderParams, decode_batch, encode_batch, row_stride
 
