@@ -876,6 +876,9 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
         }
     }
     NSG_STAMP(p, b, lane, 2);
+#if NSG_CODER_TAIL_PRIO
+    __builtin_amdgcn_s_setprio(NSG_CODER_TAIL_PRIO);  // the tail is a latency-bound chain: issue priority
+#endif
     if constexpr (NSPLIT > 1) {
         // hand the slice results to wave 0: fast-sum partials (reduced per wave, added in wave order) and the
         // candidate buffers (copied into wave 0's, converted to keys; compacted to the top-K when full)
@@ -1083,14 +1086,15 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     int k = k0 < 2 ? 2 : k0;
     if (k > p.topk) k = p.topk;
 
-    // E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
-    double el = 0.0;
+    // E = sum_{i<k} e_i, order-free (exact limb sums, canonical step 6)
+    Mass ms{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s = 0; s < NSK; ++s) {
         const int i = s * WAVE + lane;
-        if (s < nsk && i < k) el += e[s];
+        if (s < nsk && i < k) mass_add(ms, e[s]);
     }
-    const double E = wave_sum_butterfly(el);
+    mass_wave_sum(ms);
+    const double E = mass_value(ms);
 
     // q, inclusive prefix, overfill trim
     int64_t cum[NSK];

@@ -161,6 +161,46 @@ __device__ __forceinline__ double wave_sum_butterfly(double v) {
     v = v + xor_lane_f64<1>(v);
     return v;
 }
+// ---- order-free kept mass E (canonical step 6, oracle or_kept_mass): e in [0,1] cut into four 36-bit limbs
+// (truncated at 2^-120); limb sums are integers < 2^53, exact in float64 in ANY order, so no rank order is needed
+struct Mass {
+    double a, b, c, d;
+};
+__device__ __forceinline__ void mass_add(Mass& s, double e) {
+    double t = e * 0x1p12;
+    const double a = __builtin_floor(t);
+    t = (t - a) * 0x1p36;
+    const double b = __builtin_floor(t);
+    t = (t - b) * 0x1p36;
+    const double c = __builtin_floor(t);
+    t = (t - c) * 0x1p36;
+    s.a += a;
+    s.b += b;
+    s.c += c;
+    s.d += __builtin_floor(t);
+}
+__device__ __forceinline__ void mass_wave_sum(Mass& s) {  // exact: every lane ends with the wave's sums
+    s.a = wave_sum_butterfly(s.a);
+    s.b = wave_sum_butterfly(s.b);
+    s.c = wave_sum_butterfly(s.c);
+    s.d = wave_sum_butterfly(s.d);
+}
+__device__ __forceinline__ double mass_value(Mass s) {  // normalise (carries), then the canonical roundings
+    double q = __builtin_floor(s.d * 0x1p-36);
+    s.d -= q * 0x1p36;
+    s.c += q;
+    q = __builtin_floor(s.c * 0x1p-36);
+    s.c -= q * 0x1p36;
+    s.b += q;
+    q = __builtin_floor(s.b * 0x1p-36);
+    s.b -= q * 0x1p36;
+    s.a += q;
+    double t = s.d * 0x1p-120;
+    t = __builtin_fma(s.c, 0x1p-84, t);  // products by powers of two are exact: fma == mul + add here
+    t = __builtin_fma(s.b, 0x1p-48, t);
+    return __builtin_fma(s.a, 0x1p-12, t);
+}
+
 // value of lane `src` (wave-uniform) in every lane: two v_readlane, no LDS
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int src) {
     src = __builtin_amdgcn_readfirstlane(src);  // the callers' lane index is uniform (ballot-derived)

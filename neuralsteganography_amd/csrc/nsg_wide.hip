@@ -381,6 +381,33 @@ __device__ RowStats block_row_stats(const StepParams& p, const char* rowc, doubl
     return rs;
 }
 
+// the kept mass E of ranks [0, k) (exact limb sums: any split over threads gives the same value); every
+// thread of the block gets it
+template <int NT = WIDE_THREADS, typename EOf>
+__device__ double block_mass(int k, EOf e_of, double* sm64) {
+    Mass ms{0.0, 0.0, 0.0, 0.0};
+    for (int i = (int)threadIdx.x; i < k; i += NT) mass_add(ms, e_of(i));
+    mass_wave_sum(ms);
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane == 0) {
+        sm64[4 * wv + 0] = ms.a;
+        sm64[4 * wv + 1] = ms.b;
+        sm64[4 * wv + 2] = ms.c;
+        sm64[4 * wv + 3] = ms.d;
+    }
+    __syncthreads();
+    Mass t{0.0, 0.0, 0.0, 0.0};
+    for (int w = 0; w < NT / WAVE; ++w) {
+        t.a += sm64[4 * w + 0];
+        t.b += sm64[4 * w + 1];
+        t.c += sm64[4 * w + 2];
+        t.d += sm64[4 * w + 3];
+    }
+    __syncthreads();
+    return mass_value(t);
+}
+
 // interval update, bit emit and state/statistics writes of one finished step (thread 0; both CDF kernels)
 template <bool DECODE>
 __device__ __forceinline__ void wide_finish(const StepParams& p, int b, const ns_stream_state& st, int k, int kp, int sel, bool exact,
@@ -571,18 +598,8 @@ __device__ __forceinline__ void wide_cdf_stream(const StepParams& p, const WideS
     int k = k0 < 2 ? 2 : k0;
     if (k > p.topk) k = p.topk;
 
-    // ---- 2. E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
-    double acc = 0.0;
-    for (int base = 0; base < k; base += WIDE_ROUND) {
-        for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < k) ? e_of(base + i) : 0.0;
-        __syncthreads();
-        if (tid < 64)
-            for (int i = tid; i < WIDE_ROUND && base + i < k; i += 64) acc += ebuf[i];
-        __syncthreads();
-    }
-    if (tid < 64) sm64[tid] = acc;
-    __syncthreads();
-    const double E = block_canonical_butterfly(sm64);
+    // ---- 2. E = sum_{i<k} e_i, order-free (exact limb sums, canonical step 6)
+    const double E = block_mass(k, e_of, sm64);
 
     // ---- 3. q_i = rint(e_i/E*R), inclusive prefix over contiguous rank chunks, overfill trim
     const int cs = (k + WIDE_THREADS - 1) / WIDE_THREADS;
@@ -1030,24 +1047,9 @@ __device__ __forceinline__ void fast_tail(const StepParams& p, const WideStat& w
         defer();
         return;
     }
-    // ---- 2. E = sum_{i<k} e_i, canonical (rank i -> lane i&63, per-lane increasing, butterfly)
+    // ---- 2. E = sum_{i<k} e_i, order-free (exact limb sums, canonical step 6)
     double* s_d = (double*)(s_aux + 32);
-    if (wv == 0) {
-        double acc = 0.0;
-        int i = lane;
-        for (; i + 7 * WAVE < k; i += 8 * WAVE) {
-            double t[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = s_e[i + u * WAVE];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc += t[u];
-        }
-        for (; i < k; i += WAVE) acc += s_e[i];
-        acc = wave_sum_butterfly(acc);
-        if (lane == 0) s_d[0] = acc;
-    }
-    __syncthreads();
-    const double E = s_d[0];
+    const double E = block_mass<FAST_THREADS>(k, [&](int i) { return s_e[i]; }, s_d);
     // ---- 3. q_i = rint(e_i/E*R); inclusive prefix in rank order (wave scans + per-round wave totals)
     const int nr = (k + FAST_THREADS - 1) / FAST_THREADS;
     int64_t* s_tot = (int64_t*)(s_aux + 64);  // [FAST_R][FAST_WAVES]
@@ -1474,6 +1476,9 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_sc
 #ifndef NSG_WIDE_ONEPASS
 #define NSG_WIDE_ONEPASS 1
 #endif
+#ifndef NSG_TAIL_PRIO
+#define NSG_TAIL_PRIO 0  // s_setprio level of the one-pass kernel after its row stream (0: off)
+#endif
 #ifndef NSG_OP_RING
 #define NSG_OP_RING 4
 #endif
@@ -1521,7 +1526,322 @@ __device__ __forceinline__ int wave_compact(uint64_t* wbuf, int cnt, float t) {
     return __builtin_amdgcn_readfirstlane(nc);
 }
 
+// ---- sort-free tail (round 3) -------------------------------------------------------------------------------
+// The CDF needs the kept keys' q_i in rank order only where a cumulative sum is SEARCHED (the overfill trim,
+// the selection, the received token's interval), and E no longer needs any order (canonical step 6).  So the
+// usual stream is finished without sorting its ~4,000 kept keys:
+//   1. every thread: its keys' exps and kept flags (not provably below the cutoff); wave sums of the limb mass,
+//      the kept count, the key range, an ambiguity flag -> one barrier -> E, k
+//   2. q_i and a 512-bucket histogram (monotone in the key: bucket order = rank order) of counts and q sums
+//      (LDS atomics) -> exclusive prefix per bucket (one bucket per thread, wave scans) -> the overfill bucket
+//   3. the kept keys scattered in bucket order (unordered inside a bucket)
+//   4. wave 0 ranks the few keys of the searched buckets among themselves (<= 64 each: lane-to-lane loop) and
+//      finishes the step: overfill trim, selection (encode) or the received token's rank (decode)
+// Anything else -- an ambiguous cutoff, k outside [2, topk], a bucket with more than 64 keys, a decode token that is
+// not kept or sits in the overfill bucket, statistics, the sampler -- returns false BEFORE s_keys is touched, and
+// the stream takes fast_tail (sort) as before.  Same integers: the kept set, E and every q_i are the canonical
+// step's; the searches give the first rank whose cumulative sum crosses the target, as the rank-order scans do.
+#ifndef NSG_NOSORT
+#define NSG_NOSORT 0  // sort-free tail (A/B: see DESIGN.md)
+#endif
+constexpr int NS_NB = FAST_THREADS;  // buckets (one per thread in the scan)
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = shfl_xor_u64(v, off);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = shfl_xor_u64(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct KeysWave {  // slot r of a thread: entry r * 64 + lane of its wave's raw LDS buffer
+    const uint64_t* wbuf;
+    int mine;
+    __device__ __forceinline__ bool operator()(int r, uint64_t& key) const {
+        const int j = r * WAVE + (int)(threadIdx.x & (WAVE - 1));
+        key = j < mine ? op_raw_key(wbuf[j]) : 0ull;
+        return j < mine;
+    }
+};
+
+// own function (not inlined): its register demand stays out of the row-stream loop's allocation
 template <typename T, bool DECODE>
+__device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* wsb, const int b, const KeysWave kin,
+                                         uint64_t* s_keys, uint64_t* s_aux) {
+    const WideStat w = *wsb;
+    const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    uint64_t* qb = s_aux;                       // [NS_NB] bucket q sums, then their exclusive prefix
+    uint32_t* cb = (uint32_t*)(s_aux + NS_NB);  // [NS_NB] bucket counts, then their exclusive prefix
+    uint64_t* pw = s_aux + NS_NB + NS_NB / 2;   // 256 words of per-wave partials
+    const ns_stream_state st = p.state[b];
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R, thr = 1.0 / Rd;
+    const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15)), inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
+    const double m = (double)w.m;  // the row max = the largest collected key's value
+    // ---- 1. exps, kept flags, limb mass, key range (keys re-read from LDS in every phase and exps recomputed
+    // in step 2: register arrays of all slots would spill at the 80-VGPR occupancy budget)
+    auto e_of = [&](uint64_t k) __attribute__((always_inline)) -> double {
+        return exp_canon(((double)wkey_val(k) - m) * p.inv_temp);
+    };
+    uint32_t vm = 0u, km = 0u;
+    Mass ms{0.0, 0.0, 0.0, 0.0};
+    uint64_t kmin = ~0ull, kmax = 0ull;
+    uint32_t nk = 0u;
+    bool amb = false;
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        uint64_t k;
+        if (!kin(r, k)) continue;
+        vm |= 1u << r;
+        kmax = k > kmax ? k : kmax;
+        const double e = e_of(k);
+        if (e * inv_lo < thr) continue;  // provably below the cutoff
+        amb |= !(e * inv_hi >= thr);     // neither provably below nor above: the exact sum decides
+        km |= 1u << r;
+        ++nk;
+        kmin = k < kmin ? k : kmin;
+        mass_add(ms, e);
+    }
+    mass_wave_sum(ms);
+    kmin = wave_min_u64(kmin);
+    kmax = wave_max_u64(kmax);
+    nk = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(nk), WAVE - 1);
+    const bool wamb = ballot(amb) != 0ull;
+    if (lane == 0) {
+        pw[8 * wv + 0] = __builtin_bit_cast(uint64_t, ms.a);
+        pw[8 * wv + 1] = __builtin_bit_cast(uint64_t, ms.b);
+        pw[8 * wv + 2] = __builtin_bit_cast(uint64_t, ms.c);
+        pw[8 * wv + 3] = __builtin_bit_cast(uint64_t, ms.d);
+        pw[8 * wv + 4] = kmin;
+        pw[8 * wv + 5] = kmax;
+        pw[8 * wv + 6] = (uint64_t)nk | ((uint64_t)(wamb ? 1u : 0u) << 32);
+    }
+    __syncthreads();
+    Mass tot{0.0, 0.0, 0.0, 0.0};
+    uint64_t kmin_a = ~0ull, kmax_a = 0ull;
+    int k0 = 0;
+    bool amb_a = false;
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) {
+        tot.a += __builtin_bit_cast(double, pw[8 * i + 0]);
+        tot.b += __builtin_bit_cast(double, pw[8 * i + 1]);
+        tot.c += __builtin_bit_cast(double, pw[8 * i + 2]);
+        tot.d += __builtin_bit_cast(double, pw[8 * i + 3]);
+        kmin_a = pw[8 * i + 4] < kmin_a ? pw[8 * i + 4] : kmin_a;
+        kmax_a = pw[8 * i + 5] > kmax_a ? pw[8 * i + 5] : kmax_a;
+        k0 += (int)(uint32_t)pw[8 * i + 6];
+        amb_a |= (pw[8 * i + 6] >> 32) != 0ull;
+    }
+    // decode: the received token must be a kept key (else fast_tail reports the divergence + ranked export)
+    uint64_t kt = 0ull;
+    if (DECODE) {
+        const int32_t tok = p.in_token[b];
+        if (tok >= 0 && tok < p.V && !is_banned(p, tok)) {
+            const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+            kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+        }
+    }
+    if (amb_a || k0 < 2 || k0 > p.topk || (DECODE && !(kt >= kmin_a && kt <= kmax_a))) return false;
+    const double E = mass_value(tot);
+    NSG_STAMP(p, b, tid, 5);
+    // ---- 2. q and the bucket histogram (bucket 0 = the largest keys; monotone, so bucket order = rank order)
+    qb[tid] = 0ull;
+    cb[tid] = 0u;
+    __syncthreads();
+    const double bscale = (double)NS_NB / ((double)(kmax_a - kmin_a) + 1.0);
+    auto bucket_of = [&](uint64_t k) __attribute__((always_inline)) -> uint32_t {
+        return min((uint32_t)((double)(kmax_a - k) * bscale), (uint32_t)(NS_NB - 1));
+    };
+    uint32_t bs[FAST_R];
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        bs[r] = 0u;
+        if ((km >> r) & 1u) {
+            uint64_t k;
+            kin(r, k);
+            const int64_t q = (int64_t)__builtin_rint((e_of(k) / E) * Rd);
+            const uint32_t bk = bucket_of(k);
+            bs[r] = (bk << 16) | atomicAdd(&cb[bk], 1u);
+            atomicAdd((unsigned long long*)&qb[bk], (unsigned long long)q);
+        }
+    }
+    __syncthreads();
+    // ---- 3. exclusive prefixes (thread t owns bucket t), the largest bucket, the overfill bucket
+    const uint32_t c = cb[tid];
+    const int64_t qv = (int64_t)qb[tid];
+    const uint32_t ci = wave_incl_scan_u32(c);
+    const int64_t qi = wave_incl_scan(qv, lane);
+    uint32_t occ = c;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) occ = max(occ, (uint32_t)__shfl_xor((int)occ, off));
+    if (lane == WAVE - 1) {
+        pw[64 + wv] = (uint64_t)qi;
+        pw[72 + wv] = (uint64_t)ci | ((uint64_t)occ << 32);
+    }
+    __syncthreads();
+    int64_t qbefore = 0, Q = 0;
+    uint32_t cbefore = 0u, maxocc = 0u;
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) {
+        const int64_t tq = (int64_t)pw[64 + i];
+        const uint32_t tc = (uint32_t)pw[72 + i];
+        if (i < wv) {
+            qbefore += tq;
+            cbefore += tc;
+        }
+        Q += tq;
+        maxocc = max(maxocc, (uint32_t)(pw[72 + i] >> 32));
+    }
+    if (maxocc > (uint32_t)WAVE) return false;  // a crowded bucket (skewed row): the sort path
+    NSG_STAMP(p, b, tid, 6);
+    const int64_t QP = qbefore + qi - qv;        // exclusive prefix of bucket tid
+    const uint32_t CP = cbefore + ci - c;
+    // overfill bucket: the first whose inclusive prefix exceeds R (NS_NB: none)
+    int ovf = (Q > (int64_t)R && QP + qv > (int64_t)R) ? tid : NS_NB;
+    ovf = wave_min_int(ovf);
+    // the decode token's bucket must lie before the overfill bucket (else the sort path checks it)
+    const int bt = DECODE ? (int)bucket_of(kt) : 0;
+    __syncthreads();  // every thread has read its bucket's count and sum
+    qb[tid] = (uint64_t)QP;
+    cb[tid] = CP;
+    if (lane == 0) pw[80 + wv] = (uint64_t)(uint32_t)ovf;
+    __syncthreads();
+    int b_ov = NS_NB;
+#pragma unroll
+    for (int i = 0; i < FAST_WAVES; ++i) b_ov = min(b_ov, (int)(uint32_t)pw[80 + i]);
+    if (DECODE && bt >= b_ov) return false;
+    // ---- 4. kept keys in bucket order: every thread holds its keys in registers before the first write
+    uint64_t kr[FAST_R];
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r) {
+        kr[r] = 0ull;
+        if ((km >> r) & 1u) kin(r, kr[r]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < FAST_R; ++r)
+        if ((km >> r) & 1u) s_keys[cb[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = kr[r];
+    __syncthreads();
+    if (wv != 0) return true;
+    NSG_STAMP(p, b, tid, 7);
+    // ---- 5. wave 0: resolve the searched buckets and finish the step
+    // member `lane` of bucket bk: its key, q, rank among the members, and cum = inclusive prefix at its rank
+    auto resolve = [&](int bk, uint64_t& key, int64_t& q, int& rank, int64_t& cum, int& occ_b)
+                       __attribute__((always_inline)) {
+        const int c0 = (int)cb[bk], c1 = bk + 1 < NS_NB ? (int)cb[bk + 1] : k0;
+        occ_b = c1 - c0;
+        const bool valid = lane < occ_b;
+        key = valid ? s_keys[c0 + lane] : 0ull;
+        q = valid ? (int64_t)__builtin_rint((e_of(key) / E) * Rd) : 0;
+        rank = 0;
+        int64_t ge = 0;
+        for (int o = 0; o < occ_b; ++o) {
+            const uint64_t ko = readlane_u64(key, o);
+            const int64_t qo = (int64_t)readlane_u64((uint64_t)q, o);
+            rank += ko > key ? 1 : 0;
+            ge += ko >= key ? qo : 0;
+        }
+        cum = (int64_t)qb[bk] + ge;
+    };
+    int kp = k0;
+    int64_t cumkp = Q;  // cum(kp - 1)
+    int kp_local = WAVE;
+    if (b_ov < NS_NB) {
+        uint64_t key;
+        int64_t q, cum;
+        int rank, occ_b;
+        resolve(b_ov, key, q, rank, cum, occ_b);
+        const bool over = lane < occ_b && cum > (int64_t)R;
+        kp_local = wave_min_int(over ? rank : WAVE);
+        kp = (int)cb[b_ov] + kp_local;
+        // cum(kp - 1): the member ranked kp_local - 1, or the prefix before the bucket
+        const bool prev = lane < occ_b && rank == kp_local - 1;
+        const uint64_t mp = ballot(prev);
+        cumkp = mp ? (int64_t)readlane_u64((uint64_t)cum, __builtin_ctzll(mp)) : (int64_t)qb[b_ov];
+    }
+    const int64_t shift = (int64_t)R - cumkp + (int64_t)st.lo;
+    int sel = -1;
+    int64_t cum_m1 = 0, cum_sel = 0;
+    uint64_t sel_key = 0ull;
+    if (!DECODE) {
+        const uint64_t idx = payload_window(p, b, st.bit_pos);
+        // first bucket (<= b_ov) whose inclusive cum + shift exceeds idx; 8 buckets per lane
+        int bs_l = NS_NB;
+#pragma unroll
+        for (int j = 0; j < NS_NB / WAVE; ++j) {
+            const int bk = lane * (NS_NB / WAVE) + j;
+            if (bk > b_ov) break;
+            const int64_t incl = bk == b_ov ? cumkp : (bk + 1 < NS_NB ? (int64_t)qb[bk + 1] : Q);
+            if ((uint64_t)(incl + shift) > idx) {
+                bs_l = bk;
+                break;
+            }
+        }
+        const int bsel = wave_min_int(bs_l);
+        if (bsel < NS_NB) {
+            uint64_t key;
+            int64_t q, cum;
+            int rank, occ_b;
+            resolve(bsel, key, q, rank, cum, occ_b);
+            const bool hit = lane < occ_b && (bsel != b_ov || rank < kp_local) && (uint64_t)(cum + shift) > idx;
+            const int rl = wave_min_int(hit ? rank : WAVE);
+            const uint64_t mh = ballot(hit && rank == rl);
+            if (mh) {
+                const int src = __builtin_ctzll(mh);
+                sel = (int)cb[bsel] + rl;
+                cum_sel = (int64_t)readlane_u64((uint64_t)cum, src);
+                cum_m1 = cum_sel - (int64_t)readlane_u64((uint64_t)q, src);
+                sel_key = readlane_u64(key, src);
+            }
+        }
+    } else {
+        uint64_t key;
+        int64_t q, cum;
+        int rank, occ_b;
+        resolve(bt, key, q, rank, cum, occ_b);
+        const uint64_t mh = ballot(lane < occ_b && key == kt);
+        if (mh) {
+            const int src = __builtin_ctzll(mh);
+            sel = (int)cb[bt] + __builtin_amdgcn_readlane(rank, src);
+            cum_sel = (int64_t)readlane_u64((uint64_t)cum, src);
+            cum_m1 = cum_sel - (int64_t)readlane_u64((uint64_t)q, src);
+            sel_key = kt;
+        }
+    }
+    if (lane != 0) return true;
+    if (sel < 0) {  // encode: no interval above the payload index (decode cannot get here: the token is kept)
+        p.state[b].flags = st.flags | (DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE) | NS_ST_DONE;
+        if (p.trace) {
+            ns_step_trace tr = {k0, kp, -1, -1, -1, 0, w.S_fast};
+            p.trace[b] = tr;
+        }
+        return true;
+    }
+    const RowStats rs{0.0, 0.0, 0.0};
+    wide_finish<DECODE>(p, b, st, k0, kp, sel, false, w.S_fast, sel > 0 ? cum_m1 : 0, cum_sel, shift, sel_key, m, rs,
+                        0.0, false);
+    NSG_STAMP(p, b, tid, 8);
+    NSG_STAMP_RT(p, b, tid, 10);
+    return true;
+}
+
+// STATS: the encode statistics' two extra streaming sums (EncodeSession(stats=True)) -- a separate instance, so
+// the plain row stream does not carry their registers
+template <typename T, bool DECODE, bool STATS = false>
 __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_onepass_kernel(
     StepParams p, WideStat* ws, uint64_t* keys_in, uint64_t* keys_out, unsigned int* count, int cap,
     unsigned int* todo) {
@@ -1565,7 +1885,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     double* s_d = (double*)(s_aux + 16);
     int* s_n = (int*)(s_aux + 48);
     float* s_xt = (float*)(s_aux + 52);
-    const bool stats = p.stats != nullptr;
+    constexpr bool stats = STATS;
     const double temp = 1.0 / p.inv_temp;
     const float tempf = (float)temp;
     const double Rd = (double)(st.hi - st.lo);
@@ -1783,6 +2103,11 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     return;
 #endif
     NSG_STAMP(p, b, tid, 2);
+#if NSG_TAIL_PRIO
+    // the rest of the step is a latency-bound chain of block reductions, barriers and fp64 work, sharing its SIMDs
+    // with the row streams of the other resident workgroups: give it issue priority
+    __builtin_amdgcn_s_setprio(NSG_TAIL_PRIO);
+#endif
 
     // ---- the row's statistics
     accS = wave_sum_butterfly(accS);
@@ -1974,6 +2299,12 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
         key = i < n ? kout[i] : 0ull;
         return i < n;
     };
+#if NSG_NOSORT
+    if (from_lds && !(!DECODE && p.sample) && !w.exact && !(!DECODE && p.stats != nullptr)) {
+        if (nosort_tail<T, DECODE>(p, &ws[b], b, KeysWave{wbuf, mine}, s_keys, s_aux)) return;
+        __syncthreads();  // the partials area of s_aux is rewritten by fast_tail
+    }
+#endif
     fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, at, keys_out, cap, todo, s_keys, s_aux);
 }
 
@@ -2239,8 +2570,12 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     const int B = p.B;
     if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
 #if NSG_WIDE_ONEPASS
-    hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
-                       w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+    if (!DECODE && p.stats)
+        hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE, true>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p,
+                           w.stat, w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+    else
+        hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
+                           w.keys_in, w.keys_out, w.count, w.cap, w.todo);
 #else
     hipLaunchKernelGGL((nsg::wide_scan_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);

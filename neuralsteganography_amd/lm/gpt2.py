@@ -132,7 +132,7 @@ class BatchedGPT2:
         s = self.shape
         return 2 * s.n_layer * B * s.n_embd * torch.tensor([], dtype=self.kv_torch_dtype).element_size()
 
-    def fit_positions(self, B: int, want: int, reserve: float = 0.15) -> int:
+    def fit_positions(self, B: int, want: int, reserve: float = 0.15, count_cached: bool = True) -> int:
         """Largest cache length <= ``want`` that fits the device's free memory (keeping ``reserve`` of it for
         activations and logits).  The reference's cache is unbounded; at B = 4096 a 1 KiB payload needs ~1.1k
         positions (170 GB for GPT-2-small fp16), so the budget is sized from what is free, not guessed."""
@@ -144,11 +144,12 @@ class BatchedGPT2:
         # that cache, or the pre-touched one bench.py hands back) counts as free: reusing those segments keeps
         # the pages warm (releasing them and allocating afresh measured a much slower first pass over the new
         # cache).  When a small tensor carved out of a freed block makes the request not fit the hole (seen as a
-        # 120 GiB OOM between two encodes of different batch sizes), allocate() releases the idle segments and
-        # retries.
+        # 120 GiB OOM between two encodes of different batch sizes), _allocate_fitted releases the idle segments
+        # and sizes the cache again from what the device then reports free (count_cached=False).
         self.k_cache = self.v_cache = None
         free, _ = torch.cuda.mem_get_info(self.device)
-        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        if count_cached:
+            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
 
     def _native_buffers(self, B: int):
@@ -178,6 +179,16 @@ class BatchedGPT2:
             return kc.stride(1), kc.stride(2), kc.stride(0)
         return kc.stride(0), kc.stride(1), 0  # plain [B, H, rows, D]
 
+    def _allocate_fitted(self, B: int, base: int, want: int, T0: int = 0) -> None:
+        """allocate(B, base + fit_positions(B, want)), falling back to a fresh budget after releasing PyTorch's
+        idle segments when the cached ones are too fragmented for the request."""
+        try:
+            self.allocate(B, base + self.fit_positions(B, want), T0=T0)
+        except torch.OutOfMemoryError:
+            self.k_cache = self.v_cache = None
+            torch.cuda.empty_cache()
+            self.allocate(B, base + self.fit_positions(B, want, count_cached=False), T0=T0)
+
     def allocate(self, B: int, max_len: int, T0: int = 0, dtype=None, plain=None) -> None:
         """Per-stream KV cache for absolute positions [T0, max_len): positions below T0 (the shared context,
         native path only) live once in ``kp``/``vp`` instead of B times.  The native decode step keeps the cache
@@ -188,14 +199,8 @@ class BatchedGPT2:
         shp = self._cache_shape(B, max_len - T0, plain)
         # uninitialised: attention only ever reads positions < L + 1, all written before they are read
         kdt = self.kv_torch_dtype if dtype is None else dtype
-        try:
-            self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
-            self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
-        except torch.OutOfMemoryError:  # idle cached segments too fragmented for the request: release, retry once
-            self.k_cache = self.v_cache = None
-            torch.cuda.empty_cache()
-            self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
-            self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
+        self.k_cache = torch.empty(shp, device=self.device, dtype=kdt)
+        self.v_cache = torch.empty(shp, device=self.device, dtype=kdt)
         self.B, self.L, self.max_len, self.T0 = B, 0, max_len, T0
         if T0 == 0:
             self.kp = self.vp = None
@@ -295,10 +300,10 @@ class BatchedGPT2:
                 kp, vp = self._quantize_fp8(kp), self._quantize_fp8(vp)
             # the one-stream prefill cache survives as kp/vp: it is not free memory for the stream cache
             self.k_cache = self.v_cache = None
-            self.allocate(B, T + self.fit_positions(B, max_new), T0=T)
+            self._allocate_fitted(B, T, max_new, T0=T)
             self.kp, self.vp = kp, vp
         else:
-            self.allocate(B, self.fit_positions(B, T + max_new))
+            self._allocate_fitted(B, 0, T + max_new)
             if self.max_len < T + 1:
                 raise RuntimeError(f"no device memory for a {T + 1}-position KV cache at B={B}")
             # run the context for one stream, then copy its cache to every stream

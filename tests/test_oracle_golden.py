@@ -205,3 +205,32 @@ def test_oracle_rank_coder_over_generic_providers_matches_reference(name):
         assert toks == s.tokens and cons == s.consumed, f"{name} stream {s.stream}"
         dec = oracle.rank_decode_stream(row, toks, cons, 8 * len(s.payload), temp=1.0, quality=m["quality"])
         assert dec == s.payload == s.decoded
+
+
+def test_kept_mass_is_order_free_and_accurate():
+    """Canonical step 6 (round 3): E is computed from exact 36-bit limb sums, so every order of the terms gives
+    the same bits (a kernel may add them in any order, no sort needed), and it is the float64 sum to ~2 ulp."""
+    import ctypes
+    import math
+
+    import numpy as np
+
+    from oracle import oracle
+
+    L = oracle.lib()
+    f = L.or_kept_mass
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    rng = np.random.default_rng(7)
+    for n, scale in [(2, 1.0), (300, 3.0), (5000, 3.0), (60000, 1.0), (4000, 40.0)]:
+        x = -np.abs(rng.standard_normal(n)) * scale
+        e = np.array([oracle.exp_canon(float(v)) for v in x], dtype=np.float64)
+        e[0] = 1.0
+        vals = set()
+        for _ in range(4):
+            p = np.ascontiguousarray(rng.permutation(e))
+            vals.add(f(p.ctypes.data, n))
+        assert len(vals) == 1
+        E = vals.pop()
+        ref = math.fsum(e.tolist())
+        assert abs(E - ref) <= 4 * math.ulp(ref)
