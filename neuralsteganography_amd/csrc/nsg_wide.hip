@@ -1839,9 +1839,7 @@ __device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* ws
     return true;
 }
 
-// STATS: the encode statistics' two extra streaming sums (EncodeSession(stats=True)) -- a separate instance, so
-// the plain row stream does not carry their registers
-template <typename T, bool DECODE, bool STATS = false>
+template <typename T, bool DECODE>
 __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_onepass_kernel(
     StepParams p, WideStat* ws, uint64_t* keys_in, uint64_t* keys_out, unsigned int* count, int cap,
     unsigned int* todo) {
@@ -1885,7 +1883,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     double* s_d = (double*)(s_aux + 16);
     int* s_n = (int*)(s_aux + 48);
     float* s_xt = (float*)(s_aux + 52);
-    constexpr bool stats = STATS;
+    const bool stats = p.stats != nullptr;
     const double temp = 1.0 / p.inv_temp;
     const float tempf = (float)temp;
     const double Rd = (double)(st.hi - st.lo);
@@ -2570,12 +2568,8 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     const int B = p.B;
     if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
 #if NSG_WIDE_ONEPASS
-    if (!DECODE && p.stats)
-        hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE, true>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p,
-                           w.stat, w.keys_in, w.keys_out, w.count, w.cap, w.todo);
-    else
-        hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
-                           w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+    hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
+                       w.keys_in, w.keys_out, w.count, w.cap, w.todo);
 #else
     hipLaunchKernelGGL((nsg::wide_scan_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);
