@@ -1476,6 +1476,9 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_sc
 #ifndef NSG_WIDE_ONEPASS
 #define NSG_WIDE_ONEPASS 1
 #endif
+#ifndef NSG_WIDE_SPLIT
+#define NSG_WIDE_SPLIT 0  // 1: row stream and tail in two kernels (wide_onepass_kernel + wide_tail_kernel)
+#endif
 #ifndef NSG_TAIL_PRIO
 #define NSG_TAIL_PRIO 0  // s_setprio level of the one-pass kernel after its row stream (0: off)
 #endif
@@ -1542,7 +1545,7 @@ __device__ __forceinline__ int wave_compact(uint64_t* wbuf, int cnt, float t) {
 // the stream takes fast_tail (sort) as before.  Same integers: the kept set, E and every q_i are the canonical
 // step's; the searches give the first rank whose cumulative sum crosses the target, as the rank-order scans do.
 #ifndef NSG_NOSORT
-#define NSG_NOSORT 0  // sort-free tail (A/B: see DESIGN.md)
+#define NSG_NOSORT 0  // sort-free tail (measured slower, A/B: DESIGN.md)
 #endif
 constexpr int NS_NB = FAST_THREADS;  // buckets (one per thread in the scan)
 
@@ -1579,8 +1582,8 @@ struct KeysWave {  // slot r of a thread: entry r * 64 + lane of its wave's raw 
 };
 
 // own function (not inlined): its register demand stays out of the row-stream loop's allocation
-template <typename T, bool DECODE>
-__device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* wsb, const int b, const KeysWave kin,
+template <typename T, bool DECODE, typename KeyAt>
+__device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* wsb, const int b, const KeyAt kin,
                                          uint64_t* s_keys, uint64_t* s_aux) {
     const WideStat w = *wsb;
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
@@ -2246,7 +2249,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
     };
 
-    int n = 0;
+    int n = 0, n_before = 0;
     bool from_lds = false;
     if (!any_ovf) {
         // ---- each wave filters its buffer to x >= xt_all in place; fast_tail reads the kept keys of its own
@@ -2256,7 +2259,10 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
         if (lane == 0) s_n[wv] = cnt;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < FAST_WAVES; ++i) n += s_n[i];
+        for (int i = 0; i < FAST_WAVES; ++i) {
+            if (i < wv) n_before += s_n[i];
+            n += s_n[i];
+        }
         __syncthreads();
         from_lds = n >= 2 || n >= V - p.nbanned;
         // fewer than two ids clear the threshold (a peaked row: k >= 2 needs the second largest, which the
@@ -2286,6 +2292,14 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     if (tid == 0) count[b] = (unsigned int)n;
     static_assert(FAST_R * WAVE == OP_CAPW, "one slot per buffer entry");
     NSG_STAMP(p, b, tid, 4);
+#if NSG_WIDE_SPLIT
+    // split form: the kept keys go to the stream's global segment (wave w's after those of waves < w) and
+    // wide_tail_kernel finishes the step, so this kernel carries no tail code (registers: the row stream only)
+    if (from_lds && n <= FAST_NL) {
+        for (int i = lane; i < cnt; i += WAVE) kout[n_before + i] = op_raw_key(wbuf[i]);
+    }
+    return;
+#endif
     const int mine = cnt;
     auto at = [&](int rr, uint64_t& key) __attribute__((always_inline)) -> bool {
         if (from_lds) {  // block-uniform
@@ -2304,6 +2318,36 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
     }
 #endif
     fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, at, keys_out, cap, todo, s_keys, s_aux);
+}
+
+// ------------------------------------------------------------------------------------------ split-form tail
+// (round 3) The tail of the one-pass step as its own kernel: one 512-thread workgroup per stream reads the kept
+// keys wide_onepass_kernel wrote to the stream's segment and runs the sort-free tail, or the LDS sort tail
+// (fast_tail, exact row sum included) when the sort-free one does not apply.  Streams the one-pass kernel
+// handed to the device-wide sort (ws.pad) and inactive streams are skipped.  Without the row stream in the
+// same kernel the tail keeps its registers (no spills at the 80-VGPR budget of three workgroups per CU) and
+// never holds a row-stream slot.
+#ifndef NSG_TAIL_WAVES_PER_SIMD
+#define NSG_TAIL_WAVES_PER_SIMD 4  // 128 VGPRs: the tail's per-slot register arrays fit without spilling
+#endif
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(FAST_THREADS, NSG_TAIL_WAVES_PER_SIMD) void wide_tail_kernel(
+    StepParams p, WideStat* ws, const uint64_t* keys_in, uint64_t* keys_out, const unsigned int* count, int cap,
+    unsigned int* todo) {
+    __shared__ uint64_t s_keys[FAST_NL];
+    __shared__ uint64_t s_aux[FAST_NB / 2];
+    const int b = blockIdx.x;
+    const WideStat w = ws[b];
+    if (!w.active || w.pad) return;
+    const int n = (int)count[b];
+    const KeysFlat kin{keys_in + (int64_t)b * cap, n};
+#if NSG_NOSORT
+    if (!(!DECODE && p.sample) && !w.exact && !(!DECODE && p.stats != nullptr)) {
+        if (nosort_tail<T, DECODE>(p, &ws[b], b, kin, s_keys, s_aux)) return;
+        __syncthreads();  // the partials area of s_aux is rewritten by fast_tail
+    }
+#endif
+    fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, kin, keys_out, cap, todo, s_keys, s_aux);
 }
 
 // ------------------------------------------------------------------------------------------ rank coder
@@ -2570,6 +2614,10 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
 #if NSG_WIDE_ONEPASS
     hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+#if NSG_WIDE_SPLIT
+    hipLaunchKernelGGL((nsg::wide_tail_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
+                       w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+#endif
 #else
     hipLaunchKernelGGL((nsg::wide_scan_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);
