@@ -2339,6 +2339,7 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_TAIL_WAVES_PER_SIMD) void wide_ta
     const int b = blockIdx.x;
     const WideStat w = ws[b];
     if (!w.active || w.pad) return;
+    NSG_STAMP(p, b, (int)threadIdx.x, 11);
     const int n = (int)count[b];
     const KeysFlat kin{keys_in + (int64_t)b * cap, n};
 #if NSG_NOSORT
