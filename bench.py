@@ -65,8 +65,10 @@ def parse(argv=None):
     ap.add_argument("--no-wide", action="store_true", help="skip the api-default (wide path) side line")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the gpt2-fa geometry leg (config C4's per-GPU share: 4096 streams, V = 42,001)")
-    ap.add_argument("--c5", action="store_true",
-                    help="add the C5 per-GPU share: GPT-2-medium fp16, topk 100, 1024 streams (coder config only)")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the C5 per-GPU share: GPT-2-medium fp16, topk 100, temp 0.9, 1024 streams")
+    ap.add_argument("--no-f16-coder", action="store_true",
+                    help="skip the fp16 coder sub-benchmark (the headline's coder kernel: roofline_f16)")
     ap.add_argument("--fp8kv", action="store_true", help="add the fp8-KV-cache end-to-end side line (opt-in mode)")
     ap.add_argument("--optin-window", type=int, default=256,
                     help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
@@ -355,10 +357,16 @@ def measured_traffic(args, version):
     return best
 
 
-def coder_bench(args, rank, world, dev):
+def coder_bench(args, rank, world, dev, dtype=None, topk=None, pcie=True):
     """The coder hot path alone: K launches of ns_encode_step over B resident synthetic logit rows (a pool of
     distinct batches, far larger than the 256 MiB Infinity Cache, cycled step by step; every stream's payload
-    cursor advances for real).  Returns the sub-object, its ``roofline`` included."""
+    cursor advances for real).  Returns the sub-object, its ``roofline`` included.  ``dtype`` / ``topk``
+    override the command line (the fp16 run is the coder the headline's end-to-end step launches)."""
+    import copy
+
+    args = copy.copy(args)
+    args.dtype = dtype or args.dtype
+    args.topk = topk or args.topk
     import torch
     import torch.distributed as dist
 
@@ -442,7 +450,7 @@ def coder_bench(args, rank, world, dev):
     stream_steps = int(f1["ntokens"].sum() - f0["ntokens"].sum())
     bits = int(f1["bit_pos"].sum() - f0["bit_pos"].sum())
     sess.raise_errors()
-    pcie = None if args.no_pcie else host_logits_rate(args, sess, pool[0], stream)
+    pcie = None if (args.no_pcie or not pcie) else host_logits_rate(args, sess, pool[0], stream)
 
     bits_all, ss_all, elapsed_max, kern_ms_max = reduce_job(bits, stream_steps, elapsed, kern_ms, device=dev)
     rank_s = per_rank(elapsed, device=dev)
@@ -499,6 +507,11 @@ def main():
     coder = coder_bench(args, rank, world, dev)
     roofline = coder.pop("roofline")
     side = {}
+    roofline_f16 = None
+    if not args.no_f16_coder:  # the coder the headline's end-to-end step runs: fp16 rows from the head GEMM
+        log("fp16 coder sub-benchmark")
+        side["coder_f16"] = coder_bench(args, rank, world, dev, dtype="f16", topk=args.topk, pcie=False)
+        roofline_f16 = side["coder_f16"].pop("roofline")
     if not args.no_wide:
         log("wide path")
         side["wide_path"] = wide_path(args, rank, world, dev)
@@ -512,10 +525,11 @@ def main():
             side["end_to_end_c2"] = end_to_end(args, rank, world, dev, batch=1, decode=True)
         if not args.no_c4:  # C4's per-GPU share: gpt2-fa geometry (V = 42,001), 4096 streams
             log("C4 share end to end")
-            side["end_to_end_c4"] = end_to_end(args, rank, world, dev, model="gpt2-fa")
-        if args.c5:  # C5's per-GPU share (coder config; the quality guard runs in tests/test_gpu_northstar.py)
+            side["end_to_end_c4"] = end_to_end(args, rank, world, dev, model="gpt2-fa", decode=True)
+        if not args.no_c5:  # C5's per-GPU share: GPT-2-medium fp16, topk 100, temp 0.9, 1024 streams
             log("C5 share end to end")
-            side["end_to_end_c5"] = end_to_end(args, rank, world, dev, model="gpt2-medium", batch=1024, topk=100)
+            side["end_to_end_c5"] = end_to_end(args, rank, world, dev, model="gpt2-medium", batch=1024, topk=100,
+                                               decode=True)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             log("fp8 KV end to end")
             side["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
@@ -549,6 +563,8 @@ def main():
                               payload_bytes=args.payload_bytes),
                "cover_tokens_per_s": coder["cover_tokens_per_s"], "roofline": roofline, "coder": coder}
     out.update(side)
+    if roofline_f16 is not None:
+        out["roofline_f16"] = roofline_f16
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baselines")
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_baseline_seconds)

@@ -70,6 +70,16 @@ int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
                             int H, int D, int L0, const int32_t* d_L0, int cap, int window, void* d_out,
                             int64_t out_stride, float scale, void* hip_stream);
 
+/* Causal attention over B whole sequences of T tokens (positions 0..T-1, no cache): the prefill of the shared
+ * context (code_base/arithmetic.py:115-122, the first call), the guard's scoring forward
+ * (src/neuralstego/metrics/lm_scorer.py:121-131) and the src provider's max_context window forward
+ * (src/neuralstego/lm/arithmetic.py:45-74).  d_qkv fp16 [B*T, qkv_stride] (row b*T + t; q, k, v column blocks as in
+ * ns_decode_attention), d_out fp16 [B*T, out_stride].  Flash attention on the 16x16x32 f16 MFMA with an fp32
+ * online softmax and P rounded to fp16 for the PV product; each output row depends on its own sequence only
+ * (batch-invariant).  D must be 64. */
+int ns_seq_attention(const void* d_qkv, int64_t qkv_stride, void* d_out, int64_t out_stride, int B, int T, int H,
+                     int D, float scale, void* hip_stream);
+
 /* fp16 [n] -> fp8 e4m3fn [n] with the attention's conversion (n % 4 == 0, 8-byte aligned). */
 int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream);
 

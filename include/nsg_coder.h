@@ -45,6 +45,7 @@ extern "C" {
 
 #define NS_DTYPE_F32 0
 #define NS_DTYPE_F16 1
+#define NS_DTYPE_F64 2 /* rank coder only: rows are a provider's float64 probabilities (ns_set_rank_rows) */
 
 /* per-stream flags */
 #define NS_ST_DONE 1u         /* encode: all payload bits consumed; no further tokens are produced */
@@ -195,6 +196,19 @@ int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, co
                         const int32_t* d_keep_bits, const uint8_t* d_active, ns_stream_state* d_state,
                         uint8_t* d_out_bits, int64_t out_stride, double temp, const ns_rank_quality* quality,
                         ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream);
+
+/* Rank coder over a GENERIC next_token_probs provider (codec/types.py:41-45; codec/arithmetic.py:337-385): a
+ * context created with NS_DTYPE_F64 takes, in ns_rank_encode_step / ns_rank_decode_step, d_logits = [B, ld]
+ * float64 rows holding the provider's own ProbDist values (not logits; temp must be 1): an ndarray ProbDist by
+ * id, or a dict ProbDist's items sorted by id.  The values are ranked (value desc, position asc), filtered by
+ * the quality policy and renormalised in float64 exactly as codec/quality.py:57-105 does (numpy's own sum
+ * restated for the normalisations, crypto/quality.py:57-89 when prob_temp > 0), replacing the round-3 float32
+ * log-probability staging.  d_count: [B] entries per row (NULL: every row has `vocab` = ld-capacity entries);
+ * d_idmap: [B, idmap_stride] token id of each entry (NULL: the position is the id); dict_rows: the rows are
+ * dict ProbDists (then cap_bits runs over the kept entries only, as _arrays_to_dist drops zeros).  The pointers
+ * stay registered for later steps; vocab (the row capacity) must be < 131072, ids are any int32. */
+int ns_set_rank_rows(ns_ctx* ctx, const int32_t* d_count, const int32_t* d_idmap, int64_t idmap_stride,
+                     int dict_rows);
 
 /* next_token_probs of the src distribution providers (codec/distribution.py:107-142, lm/arithmetic.py:45-74):
  * d_probs [B, probs_stride] float64 receives, by token id, softmax(logits / temp) restricted to the

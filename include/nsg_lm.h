@@ -65,6 +65,12 @@ int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe
                    const int32_t* d_L, void* d_h, int64_t ldh, const void* d_w, const void* d_b, void* d_a,
                    int64_t lda, int M, int C, float eps, void* hip_stream);
 
+/* ns_lm_embed_ln for M = B*T rows of whole sequences: row b*T + t takes position t mod n_positions (the default
+ * positions of a first forward call: the context prefill, the guard's scoring forward, the max_context window). */
+int ns_lm_embed_seq_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions, int T,
+                       void* d_h, int64_t ldh, const void* d_w, const void* d_b, void* d_a, int64_t lda, int M, int C,
+                       float eps, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,7 +18,7 @@ if os.environ.get("NSG_CODER_LIB"):
     LIB_PATH = Path(os.environ["NSG_CODER_LIB"]).resolve()
 
 NS_OK, NS_ERR_CONFIG, NS_ERR_UNSUPPORTED, NS_ERR_HIP = 0, -1, -2, -3
-NS_DTYPE_F32, NS_DTYPE_F16 = 0, 1
+NS_DTYPE_F32, NS_DTYPE_F16, NS_DTYPE_F64 = 0, 1, 2  # F64: provider probability rows (rank coder)
 NS_ST_DONE, NS_ST_ERR_RANGE, NS_ST_ERR_DIVERGE, NS_ST_EXACT_SUM = 1, 2, 4, 8
 NS_STEP_FORCE_EXACT_SUM = 1
 NS_STEP_FINISH_SENT = 16
@@ -28,11 +28,11 @@ NS_MAX_BANNED = 8
 EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_topk", "ns_set_split_max_batch",
            "ns_init_state",
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
-           "ns_rank_encode_step", "ns_rank_decode_step", "ns_token_probs",
+           "ns_rank_encode_step", "ns_set_rank_rows", "ns_rank_decode_step", "ns_token_probs",
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
            "ns_decode_attention_fp8", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
-           "ns_lm_embed_ln")
+           "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
 
 
@@ -106,6 +106,8 @@ def lib() -> ctypes.CDLL:
     L.ns_token_probs.restype = ctypes.c_int
     L.ns_token_probs.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
                                  ctypes.POINTER(NsRankQuality), vp, ctypes.c_int64, vp, vp]
+    L.ns_set_rank_rows.restype = ctypes.c_int
+    L.ns_set_rank_rows.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int]
     L.ns_set_rank_export.restype = ctypes.c_int
     L.ns_set_rank_export.argtypes = [vp, vp, ctypes.c_int]
     L.ns_set_stats.restype = ctypes.c_int
@@ -145,6 +147,10 @@ def lib() -> ctypes.CDLL:
     L.ns_set_split_max_batch.argtypes = [ci]
     L.ns_lm_embed_ln.restype = ci
     L.ns_lm_embed_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_lm_embed_seq_ln.restype = ci
+    L.ns_lm_embed_seq_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_seq_attention.restype = ci
+    L.ns_seq_attention.argtypes = [vp, i64, vp, i64, ci, ci, ci, ci, ctypes.c_float, vp]
     _lib = L
     return L
 

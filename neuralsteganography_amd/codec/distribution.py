@@ -129,54 +129,88 @@ class HipTransformersLM:
         return self._probs[0].cpu().numpy().copy()
 
 
-# probability 0 (or negative / non-finite) as a log-probability: far enough below every real entry that the
-# kernel's canonical exp gives exactly 0 (exp_canon(d) = 0 for d < -700), so the id leaves the support as the
-# reference's ``probs > 0`` mask drops it (codec/arithmetic.py:366-370); finite, so key ranges stay finite
-ZERO_LOGIT_GAP = 800.0
-
-
-def dist_to_row(dist, vocab: int) -> np.ndarray:
-    """A ProbDist (float64 ndarray by id, or ``{id: p}`` dict, ``codec/arithmetic.py:388-398``) as a float64
-    probability row of ``vocab`` entries (absent ids: 0)."""
+def dist_arrays(dist):
+    """``_dist_to_arrays`` (codec/arithmetic.py:388-398, codec/quality.py:144-158): (float64 values, int32 token
+    ids or None when the array position is the id, dict flag) -- an ndarray ProbDist by id, a dict's items sorted
+    by id."""
     if isinstance(dist, np.ndarray):
-        row = np.asarray(dist, dtype=np.float64).reshape(-1)
-        if row.size > vocab:
-            raise ConfigurationError(f"distribution over {row.size} ids for a {vocab}-id vocabulary")
-        if row.size < vocab:
-            row = np.concatenate([row, np.zeros(vocab - row.size)])
-        return row
+        return np.ascontiguousarray(np.asarray(dist, dtype=np.float64).reshape(-1)), None, False
     if isinstance(dist, dict):
-        row = np.zeros(vocab, dtype=np.float64)
-        for tok, prob in dist.items():
-            t = int(tok)
-            if not 0 <= t < vocab:
-                raise ConfigurationError(f"token id {t} outside the {vocab}-id vocabulary")
-            row[t] = float(prob)
-        return row
+        items = sorted(dist.items())
+        ids = np.array([int(t) for t, _ in items], dtype=np.int64)
+        if ids.size and (ids.min() < -(1 << 31) or ids.max() >= (1 << 31)):
+            raise ConfigurationError("token ids must fit int32")
+        return (np.array([float(p) for _, p in items], dtype=np.float64), ids.astype(np.int32), True)
     raise TypeError(f"Unsupported probability distribution type: {type(dist)!r}")
 
 
-def dist_vocab(dist) -> int:
-    """Vocabulary size implied by one ProbDist (ndarray length, or the largest dict id + 1)."""
-    if isinstance(dist, np.ndarray):
-        return int(dist.size)
-    if isinstance(dist, dict):
-        return max((int(t) for t in dist), default=-1) + 1
-    raise TypeError(f"Unsupported probability distribution type: {type(dist)!r}")
+# the rank kernel keys positions below 2^17 (ns_create: vocab < 131072 on the wide path); ids are any int32
+MAX_ROW_ENTRIES = 0x1FFFF
 
 
-def probs_to_logits(rows: np.ndarray) -> np.ndarray:
-    """float64 probability rows -> float32 log-probability rows whose softmax (temperature 1, the rank kernel's
-    ``_ModelAdapter`` form) has the same support and the same order: log p, and ``max - ZERO_LOGIT_GAP`` for
-    entries that are not positive and finite.  Rows without positive mass stay all-equal (no capacity)."""
-    rows = np.asarray(rows, dtype=np.float64)
-    pos = np.isfinite(rows) & (rows > 0)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        lg = np.where(pos, np.log(np.where(pos, rows, 1.0)), -np.inf)
-    top = np.max(lg, axis=1, keepdims=True)
-    top = np.where(np.isfinite(top), top, 0.0)
-    lg = np.where(pos, lg, top - ZERO_LOGIT_GAP)
-    return lg.astype(np.float32)
+class ProbRows:
+    """A step's provider ProbDists staged for the rank kernel at float64 (``NS_DTYPE_F64``, ``ns_set_rank_rows``):
+    ``values`` [B, ld] float64 (the provider's own values in ``_dist_to_arrays`` order), ``count`` [B] int32
+    entries per row, ``idmap`` [B, ld] int32 token id per entry (None when every row is an ndarray: position = id),
+    ``dict_rows``; ``flags`` per row (host): negative / NaN / +inf entries, for the reference's quality errors."""
+
+    prob_rows = True
+
+    def __init__(self, dists, device, min_cols: int = 2):
+        import torch
+
+        arrs = [dist_arrays(d) for d in dists]
+        kinds = {a[2] for a in arrs}
+        self.dict_rows = True in kinds
+        self.mixed = len(kinds) > 1
+        n = max([a[0].size for a in arrs] + [int(min_cols)])
+        if n > MAX_ROW_ENTRIES:
+            raise ConfigurationError(f"a ProbDist of {n} entries exceeds the rank kernel's {MAX_ROW_ENTRIES}")
+        from ..coder import row_stride
+
+        self.ncols = n
+        ld = row_stride(n, "f64")
+        B = len(arrs)
+        vals = np.zeros((B, ld), dtype=np.float64)
+        cnt = np.zeros(B, dtype=np.int32)
+        ids = np.zeros((B, ld), dtype=np.int32) if self.dict_rows else None
+        self.neg = np.zeros(B, bool)
+        self.nan = np.zeros(B, bool)
+        self.posinf = np.zeros(B, bool)
+        for b, (v, idv, _) in enumerate(arrs):
+            m = v.size
+            vals[b, :m] = v
+            cnt[b] = m
+            if ids is not None:
+                ids[b, :m] = idv if idv is not None else np.arange(m, dtype=np.int32)
+            self.neg[b] = bool(np.any(v < 0))
+            self.nan[b] = bool(np.any(np.isnan(v)))
+            self.posinf[b] = bool(np.any(np.isposinf(v)))
+        self.values = torch.from_numpy(vals).to(device)
+        self.count = torch.from_numpy(cnt).to(device)
+        self.idmap = torch.from_numpy(ids).to(device) if ids is not None else None
+
+    def check_quality(self, q) -> None:
+        """The errors the reference's quality code raises on such rows (host check before the launch):
+        codec/quality.py:155-156 negative probabilities; a NaN kept by the filters or +inf make the
+        normalisation total non-finite (:174-178); the crypto policy normalises every row first
+        (crypto/quality.py:118-122)."""
+        from .errors import QualityConfigError
+
+        top_k, top_p, min_prob = q.top_k > 0, q.top_p > 0.0, q.min_prob >= 0.0
+        cap, crypto = q.cap_bits > 0, q.prob_temp > 0.0
+        if crypto:
+            if np.any(self.neg | self.nan | self.posinf):
+                raise QualityConfigError("Probability mass vanished during normalisation")
+            return
+        if not (top_k or top_p or min_prob or cap):
+            return
+        if np.any(self.neg):
+            raise QualityConfigError("Probabilities must be non-negative")
+        if np.any(self.posinf) or (np.any(self.nan) and not min_prob):
+            raise QualityConfigError("Probability mass vanished after filtering")
+        if cap and self.mixed:
+            raise ConfigurationError("cap_per_token_bits over a mix of dict and ndarray ProbDists in one step")
 
 
 def _declared_vocab(provider) -> int:
@@ -191,11 +225,14 @@ class ProviderBatchedLM:
     """``prefill(context, B, max_new)`` / ``step(tokens)`` over a ``next_token_probs`` provider: every stream's
     context grows by its emitted token, each step queries the provider once per stream (on the host -- that is
     the provider protocol) with the context trimmed to ``context_window`` (``_next_distribution``,
-    ``codec/arithmetic.py:337-347``), and hands the kernel ``[B, ld]`` float32 log-probability rows
-    (:func:`probs_to_logits`).  ``first`` is the distribution of ``context`` if the caller already has it (it
-    also fixes the vocabulary size)."""
+    ``codec/arithmetic.py:337-347``), and hands the rank kernel the ProbDists themselves at float64
+    (:class:`ProbRows`: ranked, filtered and renormalised on the device exactly as the reference's numpy does; the
+    round-3 float32 log-probability staging merged near-tied probabilities).  Any ids per step: a dict's ids map
+    through the row's id table and a longer row grows the coder context.  ``first`` is the distribution of
+    ``context`` if the caller already has it."""
 
     takes_full_context = True  # HipRankLM: pass the context untrimmed (no 1022-token cut, no [0] for empty)
+    prob_rows = True  # HipRankLM: the steps return ProbRows for a NS_DTYPE_F64 coder context
 
     def __init__(self, provider, context, *, context_window: Optional[int] = None, first=None, device=None):
         import torch
@@ -205,39 +242,24 @@ class ProviderBatchedLM:
         self.window = int(context_window) if context_window else None
         self._first_ctx = tuple(int(t) for t in context)
         self._first = first if first is not None else provider.next_token_probs(self._trim(self._first_ctx))
-        # a dict ProbDist names only its support: the id range is the provider's declared vocabulary
-        # (MockLM.vocab_size, a model's vocab) when it has one, else what the first distribution implies
-        V = max(dist_vocab(self._first), _declared_vocab(provider))
-        if V < 2:
-            raise ConfigurationError("the provider's distribution needs at least two token ids")
-        self.shape = SimpleNamespace(vocab=V, n_positions=0)
-        from ..coder import row_stride
-
-        self.ld = row_stride(V, "f32")
+        V = max(dist_arrays(self._first)[0].size, _declared_vocab(provider), 2)
+        self.shape = SimpleNamespace(vocab=min(V, MAX_ROW_ENTRIES), n_positions=0)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.ctxs = []
 
     def _trim(self, ctx):
         return tuple(ctx[-self.window:]) if self.window is not None and len(ctx) > self.window else tuple(ctx)
 
-    def _rows(self):
-        import torch
-
-        V = self.shape.vocab
-        out = np.full((len(self.ctxs), self.ld), -np.inf, dtype=np.float64)
-        for b, ctx in enumerate(self.ctxs):
+    def _rows(self) -> ProbRows:
+        dists = []
+        for ctx in self.ctxs:
             if ctx == self._first_ctx and self._first is not None:
-                dist = self._first
+                dists.append(self._first)
             else:
-                dist = self.provider.next_token_probs(self._trim(ctx))
-            try:
-                out[b, :V] = dist_to_row(dist, V)
-            except ConfigurationError as exc:
-                raise ConfigurationError(f"{exc} (the provider declares no vocab_size; the first distribution "
-                                         f"implied {V} ids)") from None
-        lg = np.zeros((len(self.ctxs), self.ld), dtype=np.float32)
-        lg[:, :V] = probs_to_logits(out[:, :V])
-        return torch.from_numpy(lg).to(self.device)
+                dists.append(self.provider.next_token_probs(self._trim(ctx)))
+        rows = ProbRows(dists, self.device, min_cols=self.shape.vocab)
+        self.shape.vocab = max(self.shape.vocab, rows.ncols)  # rows never narrower than the coder context
+        return rows
 
     def prefill(self, context, B: int, max_new: int):
         del max_new
@@ -251,4 +273,4 @@ class ProviderBatchedLM:
         return self._rows()
 
 
-__all__ = ["MockLM", "CachedLM", "HipTransformersLM", "ProviderBatchedLM", "dist_to_row", "probs_to_logits"]
+__all__ = ["MockLM", "CachedLM", "HipTransformersLM", "ProviderBatchedLM", "ProbRows", "dist_arrays"]

@@ -7,14 +7,17 @@ payload bit count) and errors as the reference.  ``lm`` is either
   ``_ModelAdapter`` softmax of ``lm/arithmetic.py:45-74`` is computed inside the kernel, temperature from the
   quality), or
 * ANY ``next_token_probs`` provider (the L2 protocol of ``codec/types.py:41-45``: the Zipf ``MockLM`` of
-  ``codec/distribution.py:17-37``, ``CachedLM``, a user model): its ProbDist rows (float64 arrays or ``{id: p}``
-  dicts) are queried on the host per step, staged to the device as log-probabilities
-  (:class:`~neuralsteganography_amd.codec.distribution.ProviderBatchedLM`) and ranked by the same kernel.  As in
-  the reference, only the ``top_k`` / ``top_p`` / ``min_prob`` / ``cap_per_token_bits`` keys of ``quality`` act
-  (``_apply_quality``, ``:350-363``) and the context is trimmed to ``max_context`` or the provider's
-  ``context_window`` (``_resolve_context_window``, ``:328-334``).
+  ``codec/distribution.py:17-37``, ``CachedLM``, a user model): its ProbDists (float64 arrays or ``{id: p}``
+  dicts) are queried on the host per step, staged to the device AS float64 values
+  (:class:`~neuralsteganography_amd.codec.distribution.ProbRows`, ``NS_DTYPE_F64``) and ranked, filtered and
+  renormalised by the rank kernel's provider-row form exactly as the reference's numpy does.  As in the reference,
+  only the ``top_k`` / ``top_p`` / ``min_prob`` / ``cap_per_token_bits`` keys of ``quality`` act (``_apply_quality``,
+  ``:350-363``) and the context is trimmed to ``max_context`` or the provider's ``context_window``
+  (``_resolve_context_window``, ``:328-334``).
 
-``max_context`` is accepted for ``HipRankLM`` for signature compatibility (see its KV-cache note).
+For a ``HipRankLM``, ``max_context`` (or the quality key of the same name) re-runs every stream's trimmed window
+per token, as the reference's ``_ModelAdapter`` does (``lm/arithmetic.py:45-74``; :class:`~neuralsteganography_amd.lm.
+rank.WindowedLM`).
 """
 
 from __future__ import annotations
@@ -23,7 +26,9 @@ from typing import Mapping, MutableMapping, Optional, Sequence
 
 from .errors import DecodeDivergenceError
 
-_CODEC_QUALITY_KEYS = ("top_k", "top_p", "min_prob", "cap_per_token_bits")
+# what reaches the coder for a generic provider (_apply_quality, codec/arithmetic.py:351-367), plus this build's
+# crypto policy key (crypto/arithmetic.py's _QualityControlledLM, applied by the rank kernel)
+_CODEC_QUALITY_KEYS = ("top_k", "top_p", "min_prob", "cap_per_token_bits", "prob_temp")
 
 
 def _resolve_context_window(lm, override: Optional[int]) -> Optional[int]:
@@ -47,12 +52,14 @@ def _rank_provider(lm, context, max_context):
     from .distribution import ProviderBatchedLM
 
     batched = ProviderBatchedLM(lm, list(context or []), context_window=_resolve_context_window(lm, max_context))
-    return HipRankLM(batched_lm=batched, logits_dtype="f32", max_batch=1), _CODEC_QUALITY_KEYS
+    return HipRankLM(batched_lm=batched, max_batch=1), _CODEC_QUALITY_KEYS
 
 
-def _codec_quality(quality, keys):
+def _codec_quality(quality, keys, max_context=None):
     q = dict(quality or {})
-    if keys is None:
+    if keys is None:  # HipRankLM: the provider reads every key; an explicit max_context trims its window
+        if max_context is not None and max_context > 0:
+            q["max_context"] = int(max_context)
         return q
     return {k: q[k] for k in keys if q.get(k) is not None}  # temperature etc. belong to the provider
 
@@ -66,7 +73,8 @@ def encode_with_lm(bits: bytes, lm, *, context: Sequence[int] | None = None, qua
             state["residual_bits"] = (0).to_bytes(8, byteorder="big", signed=False)
         return []
     prov, keys = _rank_provider(lm, context, max_context)
-    toks, states = prov.encode_batch_states([bit_list], list(context or []), quality=_codec_quality(quality, keys))
+    toks, states = prov.encode_batch_states([bit_list], list(context or []),
+                                            quality=_codec_quality(quality, keys, max_context))
     if state is not None:
         state["history"] = tuple(states[0]["history"])
         state["residual_bits"] = states[0]["residual_bits"]
@@ -87,7 +95,7 @@ def decode_with_lm(tokens: Sequence[int], lm, *, context: Sequence[int] | None =
         st["residual_bits"] = state["residual_bits"]
         total_bits = int.from_bytes(bytes(state["residual_bits"]), byteorder="big", signed=False)
     prov, keys = _rank_provider(lm, context, max_context)
-    bits = prov.decode_batch([list(tokens)], list(context or []), quality=_codec_quality(quality, keys),
+    bits = prov.decode_batch([list(tokens)], list(context or []), quality=_codec_quality(quality, keys, max_context),
                              states=[st])[0]
     if total_bits is not None and total_bits > sum(st["history"]):
         raise DecodeDivergenceError("Decoded bitstream shorter than expected")  # codec/arithmetic.py:222-223

@@ -53,7 +53,7 @@ class CoderParams:
     precision: int = 26
     temp: float = 0.9
     topk: int = 300
-    dtype: str = "f32"  # logits dtype: "f32" or "f16"
+    dtype: str = "f32"  # logits dtype: "f32" or "f16"; "f64": a provider's probability rows (rank coder only)
     banned: Optional[Sequence[int]] = None  # default: (vocab-1, 628) as arithmetic.py:124-125
 
     def banned_ids(self) -> List[int]:
@@ -67,12 +67,14 @@ class CoderParams:
             return _lib.NS_DTYPE_F32
         if self.dtype == "f16":
             return _lib.NS_DTYPE_F16
+        if self.dtype == "f64":
+            return _lib.NS_DTYPE_F64
         raise ConfigurationError(f"unsupported logits dtype {self.dtype!r}")
 
     @property
     def torch_dtype(self):
         torch = _torch()
-        return torch.float16 if self.dtype == "f16" else torch.float32
+        return {"f16": torch.float16, "f64": torch.float64}.get(self.dtype, torch.float32)
 
     def validate(self) -> None:
         if self.vocab < 2:
@@ -189,6 +191,25 @@ def _check_logits(ctx: "CoderContext", B: int, logits) -> None:
         raise ConfigurationError("logits must be contiguous rows on the GPU with ld >= vocab")
     if logits.device.index != ctx.device:
         raise ConfigurationError(f"logits on cuda:{logits.device.index}, coder context on cuda:{ctx.device}")
+
+
+def _rank_rows(ctx: "CoderContext", B: int, rows, q):
+    """The device matrix a rank step reads: logits as they are (checked), or a provider step's
+    :class:`~neuralsteganography_amd.codec.distribution.ProbRows` registered with ``ns_set_rank_rows`` (the
+    reference's quality errors raised on the host first)."""
+    if not getattr(rows, "prob_rows", False):
+        _check_logits(ctx, B, rows)
+        return rows
+    if ctx.params.dtype != "f64":
+        raise ConfigurationError("provider probability rows need a coder context of dtype 'f64'")
+    if rows.ncols > ctx.params.vocab:
+        raise ConfigurationError(f"a row of {rows.ncols} entries exceeds the context's {ctx.params.vocab}")
+    rows.check_quality(q)
+    _check_logits(ctx, B, rows.values)
+    idm = rows.idmap
+    ctx.check(_lib.lib().ns_set_rank_rows(ctx._h, _ptr(rows.count), _ptr(idm), idm.stride(0) if idm is not None else 0,
+                                          int(rows.dict_rows)), "ns_set_rank_rows")
+    return rows.values
 
 
 def _state_tensor(B: int, device):
@@ -659,7 +680,7 @@ class RankEncodeSession:
         self.cons = torch.zeros((self.B, cap), dtype=torch.int32, device=dev)
 
     def step(self, logits):
-        _check_logits(self.ctx, self.B, logits)
+        logits = _rank_rows(self.ctx, self.B, logits, self.q)
         rc = _lib.lib().ns_rank_encode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.payload), self.payload.stride(0),
             _ptr(self.nbits), _ptr(self.state), _ptr(self.out_token), _ptr(self.hist), _ptr(self.cons),
@@ -725,7 +746,7 @@ class RankDecodeSession:
 
     def step(self, logits) -> None:
         t = self.t
-        _check_logits(self.ctx, self.B, logits)
+        logits = _rank_rows(self.ctx, self.B, logits, self.q)
         rc = _lib.lib().ns_rank_decode_step(
             self.ctx._h, _ptr(logits), logits.stride(0), self.B, _ptr(self.tok[t]), _ptr(self.keep[t]),
             _ptr(self.act[t]), _ptr(self.state), _ptr(self.out_bits), self.out_stride, self.temp,

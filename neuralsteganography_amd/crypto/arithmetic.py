@@ -53,8 +53,12 @@ def _validate(top_k, top_p, temperature) -> None:
 
 
 def _rank_quality(top_k, top_p, temperature) -> dict:
-    """The policy as the rank kernel's quality keys.  ``prob_temp`` = 1.0 is the isclose no-op."""
+    """The policy as the rank kernel's quality keys.  ``prob_temp`` = 1.0 is the isclose no-op of the tempering
+    (the row is still normalised and filtered, quality.py:54-89); no keys at all when ``_QualityControlledLM``
+    returns the base distribution unchanged (top_k and top_p None and temperature exactly 1.0, :31-32)."""
     _validate(top_k, top_p, temperature)
+    if top_k is None and top_p is None and temperature == 1.0:
+        return {}
     q = {"prob_temp": 1.0 if math.isclose(temperature, 1.0) else float(temperature)}
     if top_k is not None:
         q["top_k"] = int(top_k)

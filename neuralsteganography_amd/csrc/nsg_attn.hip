@@ -343,6 +343,129 @@ __global__ void quantize_fp8_kernel(const _Float16* __restrict__ src, uint32_t* 
     dst[i] = pack4_fp8((float)s4[0], (float)s4[1], (float)s4[2], (float)s4[3]);
 }
 
+// ------------------------------------------------------------------------------------------ causal sequences
+// softmax(q k^T / sqrt(D) + causal mask) v over B sequences of T tokens at once: the shared-context prefill
+// (code_base/arithmetic.py:115-122, first call), the guard's scoring forward (metrics/lm_scorer.py:121-131) and
+// the max_context window forward of the src provider (lm/arithmetic.py:45-74).  Flash attention on the
+// v_mfma_f32_16x16x32_f16 matrix cores: a workgroup of 4 waves owns 64 queries of one (sequence, head), each wave
+// 16; key blocks of 64 are staged in LDS (K as [key][d], V transposed as [d][key], 16-byte chunks XOR-swizzled
+// by (row >> 1) & 7 so every ds_read_b128 of a 16-lane group hits distinct banks); per block S = K Q^T (lane
+// (r, c) holds query r's scores of keys 4c..4c+3 of each 16-key tile), an online softmax in fp32 (exp2, log2 e
+// folded into the scale), P staged through LDS as fp16, O += V^T P (lane holds dims 4c..4c+3 of each 16-dim tile
+// of query r).  A query's result depends only on its own sequence (fixed block order 0..its block, fixed MFMA
+// chains), never on B or on the other queries of the tile: batch-invariant like the decode step.
+typedef _Float16 sq_f16x4 __attribute__((ext_vector_type(4)));
+typedef float sq_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ sq_f32x4 sq_mfma(f16x8 a, f16x8 b, sq_f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int sq_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ _Float16 sq_h(float v) {  // fp32 pinned before the conversion (no fused rounding)
+    asm volatile("" : "+v"(v));
+    return (_Float16)v;
+}
+
+__global__ __launch_bounds__(256) void seq_attn_kernel(const _Float16* __restrict__ qkv, int64_t qkv_stride,
+                                                       _Float16* __restrict__ out, int64_t out_stride, int T, int H,
+                                                       float scale_log2) {
+    __shared__ __attribute__((aligned(16))) _Float16 sK[64 * ATT_D];
+    __shared__ __attribute__((aligned(16))) _Float16 sVt[ATT_D * 64];
+    __shared__ __attribute__((aligned(16))) _Float16 sP[4][16 * 64];
+    const int nqb = (T + 63) / 64;
+    const int qb = nqb - 1 - (int)(blockIdx.x % nqb);  // the longest query blocks of a pair are dispatched first
+    const int bh = (int)(blockIdx.x / nqb);
+    const int h = bh % H, b = bh / H;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, c = lane >> 4;
+    const int C = H * ATT_D;
+    const _Float16* base = qkv + (int64_t)b * T * qkv_stride + h * ATT_D;
+    const int tq = qb * 64 + wave * 16 + r;  // this lane's query (padding rows past T are computed, not stored)
+    f16x8 qf[2];
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc) qf[dc] = *(const f16x8*)(base + (int64_t)min(tq, T - 1) * qkv_stride + dc * 32 + c * 8);
+    sq_f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = sq_f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -1e30f, l = 0.0f;
+    _Float16* Pw = sP[wave];
+    for (int kb = 0; kb <= qb; ++kb) {
+        __syncthreads();  // the previous block's K / V reads are done
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int id = (int)threadIdx.x + 256 * u;
+            const int key = id >> 3, ch = id & 7;
+            const _Float16* src = base + (int64_t)min(kb * 64 + key, T - 1) * qkv_stride + ch * 8;
+            const f16x8 kv = *(const f16x8*)(src + C);
+            const f16x8 vv = *(const f16x8*)(src + 2 * C);
+            *(f16x8*)(sK + key * 64 + ((ch ^ sq_swz(key)) * 8)) = kv;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int d = ch * 8 + i;
+                sVt[d * 64 + (((key >> 3) ^ sq_swz(d)) * 8) + (key & 7)] = vv[i];
+            }
+        }
+        __syncthreads();
+        float s[4][4];
+        float mx = -1e30f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            sq_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            const int krow = kt * 16 + r;
+#pragma unroll
+            for (int dc = 0; dc < 2; ++dc)
+                acc = sq_mfma(*(const f16x8*)(sK + krow * 64 + (((dc * 4 + c) ^ sq_swz(krow)) * 8)), qf[dc], acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int key = kb * 64 + kt * 16 + 4 * c + i;
+                s[kt][i] = (key <= tq && key < T) ? acc[i] * scale_log2 : -__builtin_inff();
+                mx = fmaxf(mx, s[kt][i]);
+            }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            sq_f16x4 pv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float pe = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
+                l += pe;
+                pv[i] = sq_h(pe);
+            }
+            *(sq_f16x4*)(Pw + r * 64 + (((kt * 2 + (c >> 1)) ^ sq_swz(r)) * 8) + (c & 1) * 4) = pv;
+        }
+        m = mnew;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own P: every lane's writes have landed
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const f16x8 pf = *(const f16x8*)(Pw + r * 64 + (((ks * 4 + c) ^ sq_swz(r)) * 8));
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int drow = dt * 16 + r;
+                o[dt] = sq_mfma(*(const f16x8*)(sVt + drow * 64 + (((ks * 4 + c) ^ sq_swz(drow)) * 8)), pf, o[dt]);
+            }
+        }
+    }
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    if (tq >= T) return;
+    const float inv = 1.0f / l;
+    _Float16* orow = out + (int64_t)(b * T + tq) * out_stride + h * ATT_D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+        sq_f16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = sq_h(o[dt][i] * inv);
+        *(sq_f16x4*)(orow + dt * 16 + 4 * c) = v;
+    }
+}
+
 }  // namespace nsg
 
 template <class F>
@@ -446,5 +569,20 @@ extern "C" int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* 
     const int64_t n4 = n / 4;
     hipLaunchKernelGGL(nsg::quantize_fp8_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
                        (hipStream_t)hip_stream, (const _Float16*)d_src, (uint32_t*)d_dst, n4);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_seq_attention(const void* d_qkv, int64_t qkv_stride, void* d_out, int64_t out_stride, int B, int T,
+                                int H, int D, float scale, void* hip_stream) {
+    if (!d_qkv || !d_out || B < 1 || T < 1 || H < 1) return NS_ERR_CONFIG;
+    if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
+    if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D || (qkv_stride & 7) || (out_stride & 3) ||
+        (((uintptr_t)d_qkv | (uintptr_t)d_out) & 15u))
+        return NS_ERR_CONFIG;
+    const int64_t nwg = (int64_t)B * H * ((T + 63) / 64);
+    if (nwg > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(nsg::seq_attn_kernel, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)hip_stream,
+                       (const _Float16*)d_qkv, qkv_stride, (_Float16*)d_out, out_stride, T, H,
+                       scale * 1.4426950408889634f);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }

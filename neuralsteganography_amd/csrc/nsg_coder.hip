@@ -955,12 +955,45 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     to_keys(cand, lane);
     NSG_STAMP(p, b, lane, 4);
     if (cand.cnt > K) compact_topk(keys, cand.scr, cand.cnt, K, lane);
-    // fewer than K candidates after the exact re-stream: the row holds NaN logits (never candidates; every
-    // other valid id passes a -inf threshold).  Zero the missing keys (no stale LDS) and report a range error.
-    const bool short_row = cand.cnt < K;
+    // fewer than K candidates after the exact re-stream: only NaN and -inf logits are never offered (x > thr
+    // fails for them even at thr = -inf).  A -inf logit is a valid rank with probability 0 in the reference's
+    // softmax (masked ids: the decode's -1e10 on fp16 logits, a caller's -inf mask), so the missing ranks are the
+    // lowest valid -inf ids, appended here in id order; a row with a NaN logit reports a range error.
+    // Rare path: one more pass over the row by this wave.
+    bool short_row = cand.cnt < K;
     if (short_row) {
-        for (int i = cand.cnt + lane; i < K; i += WAVE) keys[i] = 0ull;
+        bool nan_row = false;
+        int have = cand.cnt;
+        for (int tile = 0; tile < ntiles; ++tile) {
+            float x[W];
+            Elem<T>::unpack(rd.vec(tile * WAVE + lane), x);
+            const int j0 = (tile * WAVE + lane) * W;
+            bool ninf[W];
+            uint32_t cl = 0u;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const bool ok = j0 + q < V && !is_banned(p, j0 + q);
+                nan_row = nan_row || (ok && x[q] != x[q]);
+                ninf[q] = ok && x[q] == -__builtin_inff();
+                cl += ninf[q] ? 1u : 0u;
+            }
+            const uint32_t incl = wave_incl_scan_u32(cl);
+            uint32_t at = (uint32_t)have + incl - cl;  // id order: lane-major, then q (ids j0 .. j0+W-1)
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                if (ninf[q]) {
+                    if (at < (uint32_t)K) keys[at] = make_key(-__builtin_inff(), (uint32_t)(j0 + q));
+                    ++at;
+                }
+            }
+            have += (int)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        }
+        nan_row = ballot(nan_row) != 0ull;
+        if (have > K) have = K;
+        for (int i = have + lane; i < K; i += WAVE) keys[i] = 0ull;  // no stale LDS past the valid ranks
         lds_fence();
+        cand.cnt = have;
+        short_row = nan_row || have < K;
     }
     NSG_STAMP(p, b, lane, 5);
     const int nsk = (K + WAVE - 1) / WAVE;
@@ -1442,6 +1475,7 @@ int ns_set_split_max_batch(int max_batch) {
 }
 
 int ns_max_topk(int logits_dtype) {
+    if (logits_dtype == NS_DTYPE_F64) return 0;  // provider rows: rank coder only (wide path)
     const int TS = (logits_dtype == NS_DTYPE_F16) ? nsg::WAVE * 8 : nsg::WAVE * 4;
     return nsg::CAND - TS;
 }
@@ -1450,7 +1484,7 @@ const char* ns_last_error(const ns_ctx* ctx) { return ctx ? ctx->err.c_str() : g
 
 ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision, int logits_dtype) {
     if (max_batch < 1 || vocab < 2 || max_k < 1 || precision < 1 || precision > 60 ||
-        (logits_dtype != NS_DTYPE_F32 && logits_dtype != NS_DTYPE_F16)) {
+        (logits_dtype != NS_DTYPE_F32 && logits_dtype != NS_DTYPE_F16 && logits_dtype != NS_DTYPE_F64)) {
         fail(nullptr, NS_ERR_CONFIG, "ns_create: invalid argument");
         return nullptr;
     }
@@ -1476,6 +1510,10 @@ ns_ctx* ns_create(int device, int max_batch, int vocab, int max_k, int precision
     ctx->ranked = nullptr;
     ctx->ranked_stride = 0;
     ctx->stamps = nullptr;
+    ctx->rk_count = nullptr;
+    ctx->rk_idmap = nullptr;
+    ctx->rk_idmap_stride = 0;
+    ctx->rk_dict = 0;
     const size_t cbytes = 4 * NS_COUNTER_SHARDS * sizeof(unsigned long long);
     if (hipMalloc((void**)&ctx->d_counters, cbytes) != hipSuccess || hipMemset(ctx->d_counters, 0, cbytes) != hipSuccess) {
         fail(nullptr, NS_ERR_HIP, "ns_create: hipMalloc failed");
@@ -1512,8 +1550,8 @@ static int prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, int64_
                    int topk, const int32_t* banned, int nbanned, ns_step_trace* d_trace, uint32_t flags,
                    ns_stream_state* d_state) {
     if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
-    const int W = ctx->dtype == NS_DTYPE_F16 ? 8 : 4;
-    const int esz = ctx->dtype == NS_DTYPE_F16 ? 2 : 4;
+    const int W = ctx->dtype == NS_DTYPE_F16 ? 8 : ctx->dtype == NS_DTYPE_F64 ? 2 : 4;
+    const int esz = ctx->dtype == NS_DTYPE_F16 ? 2 : ctx->dtype == NS_DTYPE_F64 ? 8 : 4;
     if (!d_logits || !d_state || B < 1 || B > ctx->max_batch) return fail(ctx, NS_ERR_CONFIG, "bad batch or pointer");
     if (ld < ctx->vocab || (ld % W) != 0) return fail(ctx, NS_ERR_CONFIG, "ld must be >= vocab and a multiple of 16 bytes");
     if (((uintptr_t)d_logits & 15u) != 0u) return fail(ctx, NS_ERR_CONFIG, "logits must be 16-byte aligned");
@@ -1586,6 +1624,8 @@ int ns_encode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const u
                    int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride, double temp, int topk,
                    const int32_t* banned, int nbanned, ns_step_trace* d_trace, uint32_t step_flags,
                    void* hip_stream) {
+    if (ctx && ctx->dtype == NS_DTYPE_F64)
+        return fail(ctx, NS_ERR_CONFIG, "ns_encode_step: a NS_DTYPE_F64 context holds provider probability rows (rank coder only)");
     nsg::StepParams p;
     int rc = prepare(ctx, p, d_logits, ld, B, temp, topk, banned, nbanned, d_trace, step_flags, d_state);
     if (rc != NS_OK) return rc;
@@ -1617,6 +1657,8 @@ int ns_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, const i
                    const uint8_t* d_is_last, const uint8_t* d_active, ns_stream_state* d_state,
                    uint8_t* d_out_bits, int64_t out_stride, double temp, int topk, const int32_t* banned,
                    int nbanned, ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream) {
+    if (ctx && ctx->dtype == NS_DTYPE_F64)
+        return fail(ctx, NS_ERR_CONFIG, "ns_decode_step: a NS_DTYPE_F64 context holds provider probability rows (rank coder only)");
     nsg::StepParams p;
     int rc = prepare(ctx, p, d_logits, ld, B, temp, topk, banned, nbanned, d_trace, step_flags, d_state);
     if (rc != NS_OK) return rc;
@@ -1639,6 +1681,8 @@ int ns_sample_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, uint64_
                    ns_stream_state* d_state, int32_t* d_out_token, int32_t* d_token_hist, int64_t hist_stride,
                    double temp, int topk, const int32_t* banned, int nbanned, double* d_stats,
                    ns_step_trace* d_trace, uint32_t step_flags, void* hip_stream) {
+    if (ctx && ctx->dtype == NS_DTYPE_F64)
+        return fail(ctx, NS_ERR_CONFIG, "ns_sample_step: a NS_DTYPE_F64 context holds provider probability rows (rank coder only)");
     if (!ctx) return fail(ctx, NS_ERR_CONFIG, "null context");
     nsg::StepParams p;
     const int tk = topk > 0 ? topk : ctx->vocab;  // sample.py: topk <= 0 keeps every id
@@ -1665,6 +1709,8 @@ static int rank_prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, i
     if (q->top_p > 1.0) return fail(ctx, NS_ERR_CONFIG, "top_p must be within (0, 1]");
     if (q->prob_temp > 0.0 && (q->cap_bits > 0 || q->min_prob >= 0.0))
         return fail(ctx, NS_ERR_CONFIG, "crypto quality (prob_temp) takes only top_k and top_p");
+    if (ctx->dtype == NS_DTYPE_F64 && temp != 1.0)
+        return fail(ctx, NS_ERR_CONFIG, "provider probability rows take no temperature (temp must be 1)");
     if (ctx->vocab > 0x1FFFF) return fail(ctx, NS_ERR_UNSUPPORTED, "rank coder: vocab must be < 131072");
     if (!ctx->wide.keys_in && nsg_wide_alloc(ctx) != NS_OK) {
         nsg_wide_free(ctx);
@@ -1680,6 +1726,13 @@ static int rank_prepare(ns_ctx* ctx, nsg::StepParams& p, const void* d_logits, i
     // crypto/quality.py:60: the temperature step runs unless math.isclose(T, 1.0) (rel_tol 1e-9)
     const double pt = q->prob_temp;
     p.rk_ptemp = (pt > 0.0 && fabs(pt - 1.0) > 1e-9 * fmax(pt, 1.0)) ? pt : 0.0;
+    p.rk_crypto = pt > 0.0 ? 1 : 0;
+    if (ctx->dtype == NS_DTYPE_F64) {
+        p.rk_count = ctx->rk_count;
+        p.rk_idmap = ctx->rk_idmap;
+        p.rk_idmap_stride = ctx->rk_idmap_stride;
+        p.rk_dict = ctx->rk_dict;
+    }
     return NS_OK;
 }
 
@@ -1726,6 +1779,8 @@ int ns_rank_decode_step(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, co
 
 int ns_token_probs(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, double temp, const ns_rank_quality* quality,
                    double* d_probs, int64_t probs_stride, ns_stream_state* d_scratch_state, void* hip_stream) {
+    if (ctx && ctx->dtype == NS_DTYPE_F64)
+        return fail(ctx, NS_ERR_CONFIG, "ns_token_probs: a NS_DTYPE_F64 context holds provider probability rows (rank coder only)");
     nsg::StepParams p;
     int rc = rank_prepare(ctx, p, d_logits, ld, B, temp, quality, nullptr, 0, d_scratch_state);
     if (rc != NS_OK) return rc;
@@ -1736,6 +1791,18 @@ int ns_token_probs(ns_ctx* ctx, const void* d_logits, int64_t ld, int B, double 
                        d_scratch_state, B, ctx->precision);
     if (!nsg_rank_launch(ctx, p, true, (hipStream_t)hip_stream))
         return fail(ctx, NS_ERR_HIP, "ns_token_probs: launch failed");
+    return NS_OK;
+}
+
+int ns_set_rank_rows(ns_ctx* ctx, const int32_t* d_count, const int32_t* d_idmap, int64_t idmap_stride,
+                     int dict_rows) {
+    if (!ctx) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_rows: null context");
+    if (ctx->dtype != NS_DTYPE_F64) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_rows: needs a NS_DTYPE_F64 context");
+    if (d_idmap && idmap_stride < ctx->vocab) return fail(ctx, NS_ERR_CONFIG, "ns_set_rank_rows: idmap stride < vocab");
+    ctx->rk_count = d_count;
+    ctx->rk_idmap = d_idmap;
+    ctx->rk_idmap_stride = d_idmap ? idmap_stride : 0;
+    ctx->rk_dict = dict_rows ? 1 : 0;
     return NS_OK;
 }
 

@@ -304,6 +304,11 @@ struct StepParams {
     double rk_ptemp;          // crypto quality LM: temperature on the probabilities (<= 0: off)
     int32_t* rk_cons;         // encode: bits consumed per token, [B][hist_stride]
     const int32_t* rk_keep;   // decode: bits to keep this step, [B]
+    int rk_crypto;            // crypto quality policy active (prob_temp > 0 given, isclose or not)
+    const int32_t* rk_count;  // f64 provider rows: entries per row [B] (nullable: V)
+    const int32_t* rk_idmap;  // f64 provider rows: token id per entry [B][rk_idmap_stride] (nullable: position)
+    int64_t rk_idmap_stride;
+    int rk_dict;              // f64 provider rows are dict ProbDists
     double* probs_out;        // ns_token_probs: filtered, renormalised p by id, [B][probs_stride]
     int64_t probs_stride;
     uint64_t* stamps;         // NSG_STAMPS diagnostic builds: s_memtime at phase boundaries, [B][16]

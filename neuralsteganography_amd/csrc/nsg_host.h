@@ -37,6 +37,8 @@ struct NsgWide {
     nsg::WideStat* stat = nullptr;  // [max_batch]
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
+    uint32_t* vals_in = nullptr;    // NS_DTYPE_F64 rank rows: array positions sorted with the 64-bit keys
+    uint32_t* vals_out = nullptr;   // [max_batch * cap]
 };
 
 struct ns_ctx {
@@ -53,6 +55,10 @@ struct ns_ctx {
     int32_t* ranked;          // decode rank export [B][ranked_stride] (ns_set_rank_export), nullable
     int ranked_stride;
     uint64_t* stamps;         // NSG_STAMPS diagnostic builds: per-stream phase stamps
+    const int32_t* rk_count;  // NS_DTYPE_F64: entries per row [B] (ns_set_rank_rows), nullable = vocab
+    const int32_t* rk_idmap;  // NS_DTYPE_F64: token id of each row entry [B][idmap_stride], nullable = position
+    int64_t rk_idmap_stride;
+    int rk_dict;              // NS_DTYPE_F64: rows are dict ProbDists (cap_bits universe, codec/quality.py:161-171)
     std::string err;
 };
 

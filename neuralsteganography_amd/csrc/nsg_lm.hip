@@ -905,11 +905,13 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
                                                        const int32_t* __restrict__ dL, f16* __restrict__ H,
                                                        int64_t ldh, const f16* __restrict__ w,
                                                        const f16* __restrict__ b, f16* __restrict__ A, int64_t lda,
-                                                       int M, int C, float eps) {
+                                                       int M, int C, float eps, int seq_T) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     if (dL) L = *dL;
-    const int pos = L % n_positions;  // code_base/arithmetic.py:44-48 (L >= 0)
+    // decode step: pos = L mod n_positions (code_base/arithmetic.py:44-48, L >= 0); whole sequences (seq_T > 0):
+    // row b*T + t is position t (the first call's default positions)
+    const int pos = seq_T > 0 ? (row % seq_T) % n_positions : L % n_positions;
     const int lane = threadIdx.x & 63, NV4 = C >> 2;
     const int tok = tokens[row];
     const bool ok = tok >= 0 && tok < V;
@@ -1146,6 +1148,22 @@ extern "C" int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const 
     if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
                        (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, L, d_L, (f16*)d_h, ldh, (const f16*)d_w,
-                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps);
+                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps, 0);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_embed_seq_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V,
+                                  int n_positions, int T, void* d_h, int64_t ldh, const void* d_w, const void* d_b,
+                                  void* d_a, int64_t lda, int M, int C, float eps, void* hip_stream) {
+    if (!d_tokens || !d_wte || !d_wpe || !d_h || !d_w || !d_b || !d_a || M <= 0 || C <= 0 || V <= 0 ||
+        n_positions <= 0 || T <= 0 || M % T)
+        return NS_ERR_CONFIG;
+    if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
+    const uintptr_t al = (uintptr_t)d_wte | (uintptr_t)d_wpe | (uintptr_t)d_h | (uintptr_t)d_w | (uintptr_t)d_b |
+                         (uintptr_t)d_a;
+    if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C) return NS_ERR_CONFIG;
+    hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
+                       (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, 0, nullptr, (f16*)d_h, ldh,
+                       (const f16*)d_w, (const f16*)d_b, (f16*)d_a, lda, M, C, eps, T);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }

@@ -2353,8 +2353,173 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_TAIL_WAVES_PER_SIMD) void wide_ta
 
 // ------------------------------------------------------------------------------------------ rank coder
 // src/neuralstego/codec/arithmetic.py:122-231 (encode_with_lm / decode_with_lm) with apply_quality /
-// cap_bits_per_token (codec/quality.py:57-141) over the _ModelAdapter softmax (lm/arithmetic.py:45-74):
-// canonical steps R1-R4 of oracle/nsg_oracle.c.  keys_sorted holds every id of the row in rank order.
+// cap_bits_per_token (codec/quality.py:57-141).  Two row forms share the quality cut (R2), the capacity cap (R3) and
+// the selection / emission (R4): wide_rank_kernel ranks the _ModelAdapter softmax of a logit row (canonical steps
+// R1-R4 of oracle/nsg_oracle.c), wide_rank64_kernel a generic provider's own float64 ProbDist (P0-P5).
+
+// R2: top_k, top_p (left-to-right cumsum over ranks [0, V), searchsorted 'left'), min_prob cut the support [0, n)
+template <class PF>
+__device__ int rank_quality_cut(const StepParams& p, int V, int n, PF&& pf, double* ebuf, int* smi, int& cut_sh,
+                                double& acc_sh) {
+    const int tid = threadIdx.x;
+    if (p.rk_top_k > 0) n = min(n, p.rk_top_k);
+    if (p.rk_top_p > 0.0) {
+        if (tid == 0) {
+            cut_sh = V;
+            acc_sh = 0.0;
+        }
+        __syncthreads();
+        for (int base = 0; base < V; base += WIDE_ROUND) {
+            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? pf(base + i) : 0.0;
+            __syncthreads();
+            if (tid == 0 && cut_sh == V) {
+                double a = acc_sh;
+                for (int i = 0; i < WIDE_ROUND && base + i < V; ++i) {
+                    a += ebuf[i];
+                    if (a >= p.rk_top_p) {
+                        cut_sh = base + i;
+                        break;
+                    }
+                }
+                acc_sh = a;
+            }
+            __syncthreads();
+            if (cut_sh != V) break;
+        }
+        n = min(n, min(cut_sh + 1, V));
+        __syncthreads();
+    }
+    if (p.rk_min_prob >= 0.0) {
+        int fm = V;
+        for (int i = tid; i < V; i += WIDE_THREADS)
+            if (i < fm && !(pf(i) >= p.rk_min_prob)) fm = i;
+        n = min(n, block_min_int(fm, smi));
+    }
+    return n;
+}
+
+// R3: cap_per_token_bits -- entropy of the renormalised support; bisect tau on softmax(log(f+1e-12)/tau) over the
+// universe of U ranks (float64, libm-equivalent log/exp: tolerance-level); returns the new support
+template <class PF>
+__device__ int rank_cap(const StepParams& p, int U, int n, PF&& pf, double* sm64, int* smi) {
+    const int tid = threadIdx.x;
+    if (!(p.rk_cap > 0 && n > 0)) return n;
+    double fl = 0.0;
+    for (int i = tid; i < n; i += WIDE_THREADS) fl += pf(i);
+    const double F = block_sum(fl, sm64);
+    double hl = 0.0;
+    for (int i = tid; i < n; i += WIDE_THREADS) {
+        const double f = pf(i) / F;
+        if (f > 0.0) hl -= f * log2(f);
+    }
+    const double H = block_sum(hl, sm64);
+    if (!(H > (double)p.rk_cap)) return n;
+    const double lf0 = log(pf(0) / F + 1e-12);
+    double low = 1e-6, high = 1.0;
+    int n_target = n;
+    for (int it = 0; it < 60; ++it) {
+        const double mid = (low + high) / 2.0;
+        const double mx = lf0 / mid;
+        double sl = 0.0, tl = 0.0;
+        int zl = U;
+        for (int i = tid; i < U; i += WIDE_THREADS) {
+            const double f = i < n ? pf(i) / F : 0.0;
+            const double a = log(f + 1e-12) / mid - mx;
+            const double c = exp(a);
+            if (c > 0.0) {
+                sl += c;
+                tl += c * a;
+            } else if (i < zl) {
+                zl = i;
+            }
+        }
+        const double s = block_sum(sl, sm64);
+        const double t = block_sum(tl, sm64);
+        const int nz = block_min_int(zl, smi);
+        const double Hc = (log(s) - t / s) / 0.6931471805599453;  // entropy of c/s in bits
+        if (Hc > (double)p.rk_cap) {
+            high = mid;
+        } else {
+            low = mid;
+            n_target = nz;
+        }
+    }
+    return n_target;
+}
+
+// R4: capacity c = floor(log2 n); encode: the next c payload bits (MSB-first per byte, zero padded) select the
+// rank, token = id_of(rank); decode: the received token's rank among the first 2^c (is_token(rank)), its first
+// keep bits emitted.  Every thread of the block calls it.
+template <bool DECODE, class IDF, class HITF>
+__device__ void rank_emit(const StepParams& p, int b, const ns_stream_state& st, int n, double S, IDF&& id_of,
+                          HITF&& is_token, int* smi) {
+    const int tid = threadIdx.x;
+    int c = 0;
+    while (c < 30 && (1 << (c + 1)) <= n) ++c;
+    if (c <= 0) {
+        if (tid == 0) p.state[b].flags = st.flags | (DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE) | NS_ST_DONE;
+        return;
+    }
+    if (!DECODE) {
+        if (tid != 0) return;
+        const int64_t nbits = p.nbits[b];
+        const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
+        uint32_t idx = 0;
+        int take = 0;
+        for (int t = 0; t < c; ++t) {
+            const int64_t bp = st.bit_pos + t;
+            uint32_t bit = 0;
+            if (bp < nbits) {
+                bit = (pl[bp >> 3] >> (7 - (bp & 7))) & 1u;
+                ++take;
+            }
+            idx = (idx << 1) | bit;
+        }
+        const int32_t token = id_of((int)idx);
+        ns_stream_state ns = st;
+        ns.bit_pos = st.bit_pos + take;
+        ns.ntokens = st.ntokens + 1;
+        if (ns.bit_pos >= nbits) ns.flags |= NS_ST_DONE;
+        p.state[b] = ns;
+        p.out_token[b] = token;
+        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
+        if (p.rk_cons && st.ntokens < p.hist_stride) p.rk_cons[(int64_t)b * p.hist_stride + st.ntokens] = take;
+        if (p.trace) {
+            ns_step_trace tr = {n, c, (int)idx, take, token, 0, S};
+            p.trace[b] = tr;
+        }
+        return;
+    }
+    const int32_t tok = p.in_token[b];
+    int found = 0x7FFFFFFF;
+    for (int i = tid; i < (1 << c); i += WIDE_THREADS)
+        if (is_token(i, tok)) found = min(found, i);
+    const int idx = block_min_int(found, smi);
+    if (tid != 0) return;
+    if (idx == 0x7FFFFFFF) {
+        p.state[b].flags = st.flags | NS_ST_ERR_DIVERGE | NS_ST_DONE;
+        return;
+    }
+    const int keep = min(max(p.rk_keep[b], 0), c);
+    uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
+    for (int t = 0; t < keep; ++t) {
+        const int64_t bp = st.bit_pos + t;
+        const uint8_t bitv = (uint8_t)((idx >> (c - 1 - t)) & 1);
+        const uint8_t m = (uint8_t)(0x80u >> (bp & 7));
+        ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | m) : (uint8_t)(ob[bp >> 3] & ~m);
+    }
+    ns_stream_state ns = st;
+    ns.bit_pos = st.bit_pos + keep;
+    ns.ntokens = st.ntokens + 1;
+    p.state[b] = ns;
+    if (p.trace) {
+        ns_step_trace tr = {n, c, idx, keep, tok, 0, S};
+        p.trace[b] = tr;
+    }
+}
+
+// Logit rows (the _ModelAdapter softmax, lm/arithmetic.py:45-74): canonical steps R1-R4 of oracle/nsg_oracle.c.
+// keys_sorted holds every id of the row in rank order.
 template <typename T, bool DECODE>
 __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, const WideStat* ws,
                                                                  const uint64_t* keys_sorted,
@@ -2413,39 +2578,7 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
     }
     auto pf = [&](int i) -> double { return crypto ? exp(log(p_of(i) + 1e-12) / Tq - a0) / Q : p_of(i); };
 
-    // R2: top_k, top_p (left-to-right cumsum, searchsorted 'left'), min_prob
-    if (p.rk_top_k > 0) n = min(n, p.rk_top_k);
-    if (p.rk_top_p > 0.0) {
-        if (tid == 0) {
-            cut_sh = V;
-            acc_sh = 0.0;
-        }
-        __syncthreads();
-        for (int base = 0; base < V; base += WIDE_ROUND) {
-            for (int i = tid; i < WIDE_ROUND; i += WIDE_THREADS) ebuf[i] = (base + i < V) ? pf(base + i) : 0.0;
-            __syncthreads();
-            if (tid == 0 && cut_sh == V) {
-                double a = acc_sh;
-                for (int i = 0; i < WIDE_ROUND && base + i < V; ++i) {
-                    a += ebuf[i];
-                    if (a >= p.rk_top_p) {
-                        cut_sh = base + i;
-                        break;
-                    }
-                }
-                acc_sh = a;
-            }
-            __syncthreads();
-            if (cut_sh != V) break;
-        }
-        n = min(n, min(cut_sh + 1, V));
-    }
-    if (p.rk_min_prob >= 0.0) {
-        int fm = V;
-        for (int i = tid; i < V; i += WIDE_THREADS)
-            if (i < fm && !(pf(i) >= p.rk_min_prob)) fm = i;
-        n = min(n, block_min_int(fm, smi));
-    }
+    n = rank_quality_cut(p, V, n, pf, ebuf, smi, cut_sh, acc_sh);
     // next_token_probs (codec/distribution.py:107-142): the quality-filtered support renormalised, by id
     if (p.probs_out) {
         const bool filtered = p.rk_top_k > 0 || p.rk_top_p > 0.0 || p.rk_min_prob >= 0.0;
@@ -2459,119 +2592,251 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_rank_kernel(StepParams p, c
         for (int i = tid; i < keep; i += WIDE_THREADS) out[wkey_id(sk[i])] = pf(i) / F;
         return;
     }
-    // R3: cap_per_token_bits -- entropy of the renormalised support; bisect tau on softmax(log(f+1e-12)/tau)
-    // over every id (float64, libm-equivalent log/exp: tolerance-level)
-    if (p.rk_cap > 0 && n > 0) {
-        double fl = 0.0;
-        for (int i = tid; i < n; i += WIDE_THREADS) fl += pf(i);
-        const double F = block_sum(fl, sm64);
-        double hl = 0.0;
-        for (int i = tid; i < n; i += WIDE_THREADS) {
-            const double f = pf(i) / F;
-            if (f > 0.0) hl -= f * log2(f);
-        }
-        const double H = block_sum(hl, sm64);
-        if (H > (double)p.rk_cap) {
-            const double lf0 = log(pf(0) / F + 1e-12);
-            double low = 1e-6, high = 1.0;
-            int n_target = n;
-            for (int it = 0; it < 60; ++it) {
-                const double mid = (low + high) / 2.0;
-                const double mx = lf0 / mid;
-                double sl = 0.0, tl = 0.0;
-                int zl = V;
-                for (int i = tid; i < V; i += WIDE_THREADS) {
-                    const double f = i < n ? pf(i) / F : 0.0;
-                    const double a = log(f + 1e-12) / mid - mx;
-                    const double c = exp(a);
-                    if (c > 0.0) {
-                        sl += c;
-                        tl += c * a;
-                    } else if (i < zl) {
-                        zl = i;
-                    }
-                }
-                const double s = block_sum(sl, sm64);
-                const double t = block_sum(tl, sm64);
-                const int nz = block_min_int(zl, smi);
-                const double Hc = (log(s) - t / s) / 0.6931471805599453;  // entropy of c/s in bits
-                if (Hc > (double)p.rk_cap) {
-                    high = mid;
+    n = rank_cap(p, V, n, pf, sm64, smi);
+    uint64_t kt = 0;  // decode: the received token's key
+    if (DECODE) {
+        const int32_t tok = p.in_token[b];
+        const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+        if (tok >= 0 && tok < p.V) kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
+    }
+    rank_emit<DECODE>(p, b, st, n, S, [&](int i) -> int32_t { return (int32_t)wkey_id(sk[i]); },
+                      [&](int i, int32_t) -> bool { return kt != 0 && sk[i] == kt; }, smi);
+}
+
+// ---- numpy's float64 sum over f(0..n-1), restated exactly (or_np_sum): 8192-element chunks added left to right,
+// each by numpy's pairwise_sum (leaves of <= 128 elements: 8 interleaved accumulators, < 8: a plain loop; larger
+// ranges split at n/2 rounded down to a multiple of 8).  Leaves are summed in parallel, thread 0 walks the tree.
+constexpr int NP_CHUNK = 8192;
+constexpr int NP_MAX_LEAVES = 2048;  // 131072 entries: 16 chunks x 64 leaves
+
+template <class F>
+__device__ double np_leaf(int a, int len, F&& f) {
+    if (len < 8) {
+        double res = 0.0;
+        for (int i = 0; i < len; ++i) res += f(a + i);
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f(a + j);
+    int i = 8;
+    for (; i < len - (len % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += f(a + i + j);
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < len; ++i) res += f(a + i);
+    return res;
+}
+
+template <class F>
+__device__ double block_np_sum(int n, F&& f, double* lsum, int* lstart, int* llen, int* nleaf_sh) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {  // leaves in depth-first, left-to-right order
+        int nl = 0;
+        for (int c0 = 0; c0 < n; c0 += NP_CHUNK) {
+            int sa[32], sl[32], sp = 0;
+            sa[0] = c0;
+            sl[0] = min(NP_CHUNK, n - c0);
+            sp = 1;
+            while (sp > 0) {
+                --sp;
+                const int a = sa[sp], len = sl[sp];
+                if (len <= 128) {
+                    lstart[nl] = a;
+                    llen[nl] = len;
+                    ++nl;
                 } else {
-                    low = mid;
-                    n_target = nz;
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    sa[sp] = a + n2;  // right half first on the stack: the left half is visited first
+                    sl[sp] = len - n2;
+                    sa[sp + 1] = a;
+                    sl[sp + 1] = n2;
+                    sp += 2;
                 }
             }
-            n = n_target;
         }
+        *nleaf_sh = nl;
     }
-    // R4: capacity, selection
-    int c = 0;
-    while (c < 30 && (1 << (c + 1)) <= n) ++c;
-    if (c <= 0) {
-        if (tid == 0) p.state[b].flags = st.flags | (DECODE ? NS_ST_ERR_DIVERGE : NS_ST_ERR_RANGE) | NS_ST_DONE;
-        return;
-    }
-    if (!DECODE) {
-        if (tid != 0) return;
-        const int64_t nbits = p.nbits[b];
-        const uint8_t* pl = p.payload + (int64_t)b * p.payload_stride;
-        uint32_t idx = 0;
-        int take = 0;
-        for (int t = 0; t < c; ++t) {
-            const int64_t bp = st.bit_pos + t;
-            uint32_t bit = 0;
-            if (bp < nbits) {
-                bit = (pl[bp >> 3] >> (7 - (bp & 7))) & 1u;
-                ++take;
+    __syncthreads();
+    const int nl = *nleaf_sh;
+    for (int k = tid; k < nl; k += WIDE_THREADS) lsum[k] = np_leaf(lstart[k], llen[k], f);
+    __syncthreads();
+    double total = 0.0;
+    if (tid == 0) {  // the same tree, combined bottom-up in the recursion's order
+        int li = 0;
+        for (int c0 = 0; c0 < n; c0 += NP_CHUNK) {
+            int lenS[32], stS[32];
+            double lS[32];
+            int sp = 0;
+            lenS[0] = min(NP_CHUNK, n - c0);
+            stS[0] = 0;
+            double ret = 0.0;
+            bool done = false;
+            while (!done) {
+                const int L = lenS[sp];
+                if (L <= 128) {
+                    ret = lsum[li++];
+                    bool descended = false;
+                    while (sp > 0 && !descended) {  // return to the parents
+                        --sp;
+                        if (stS[sp] == 1) {  // left child done: keep it, descend right
+                            lS[sp] = ret;
+                            stS[sp] = 2;
+                            int n2 = lenS[sp] / 2;
+                            n2 -= n2 % 8;
+                            lenS[sp + 1] = lenS[sp] - n2;
+                            stS[sp + 1] = 0;
+                            ++sp;
+                            descended = true;
+                        } else {
+                            ret = lS[sp] + ret;
+                        }
+                    }
+                    if (!descended) done = true;
+                } else {
+                    stS[sp] = 1;
+                    int n2 = L / 2;
+                    n2 -= n2 % 8;
+                    lenS[sp + 1] = n2;
+                    stS[sp + 1] = 0;
+                    ++sp;
+                }
             }
-            idx = (idx << 1) | bit;
+            total += ret;
         }
-        const int32_t token = (int32_t)wkey_id(sk[idx]);
-        ns_stream_state ns = st;
-        ns.bit_pos = st.bit_pos + take;
-        ns.ntokens = st.ntokens + 1;
-        if (ns.bit_pos >= nbits) ns.flags |= NS_ST_DONE;
-        p.state[b] = ns;
-        p.out_token[b] = token;
-        if (p.hist && st.ntokens < p.hist_stride) p.hist[(int64_t)b * p.hist_stride + st.ntokens] = token;
-        if (p.rk_cons && st.ntokens < p.hist_stride) p.rk_cons[(int64_t)b * p.hist_stride + st.ntokens] = take;
-        if (p.trace) {
-            ns_step_trace tr = {n, c, (int)idx, take, token, 0, S};
-            p.trace[b] = tr;
+        lsum[0] = total;
+    }
+    __syncthreads();
+    total = lsum[0];
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ uint64_t prob_key(double v) {
+    return v > 0.0 ? (uint64_t)__double_as_longlong(v) : 0ull;  // v <= 0 and NaN: never support, ranked last
+}
+
+// Generic provider rows (f64): per stream the activity check of the logit path, the entry count, and the keys
+// (value bits) with their array positions for the device-wide pair sort.
+template <bool DECODE>
+__global__ void rank64_prep_kernel(StepParams p, WideStat* ws, unsigned int* count) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    const ns_stream_state st = p.state[b];
+    bool active = !(st.flags & NS_ST_DONE);
+    if (!DECODE && active && st.bit_pos >= p.nbits[b]) {
+        p.state[b].flags = st.flags | NS_ST_DONE;
+        active = false;
+    }
+    if (DECODE && p.active && !p.active[b]) active = false;
+    int n = p.rk_count ? p.rk_count[b] : p.V;
+    n = min(max(n, 0), p.V);
+    WideStat w = {};
+    w.active = (active && n > 0) ? 1u : 0u;
+    ws[b] = w;
+    count[b] = w.active ? (unsigned int)n : 0u;
+}
+
+__global__ __launch_bounds__(256) void rank64_collect_kernel(StepParams p, const WideStat* ws, uint64_t* keys,
+                                                             uint32_t* vals, const unsigned int* count, int cap) {
+    const int b = blockIdx.y;
+    if (!ws[b].active) return;
+    const int n = (int)count[b];
+    const double* row = (const double*)p.logits + (int64_t)b * p.ld;
+    for (int j = blockIdx.x * COLLECT_CHUNK + (int)threadIdx.x; j < min(n, (int)(blockIdx.x + 1) * COLLECT_CHUNK);
+         j += 256) {
+        keys[(int64_t)b * cap + j] = prob_key(row[j]);
+        vals[(int64_t)b * cap + j] = (uint32_t)j;
+    }
+}
+
+// Provider rows: canonical steps P0-P5 of oracle/nsg_oracle.c (or_rank_step64).  keys_sorted / pos_sorted: the
+// row's entries in rank order (value bits desc, position asc: the pair sort is stable).
+template <bool DECODE>
+__global__ __launch_bounds__(WIDE_THREADS) void wide_rank64_kernel(StepParams p, const WideStat* ws,
+                                                                   const uint64_t* keys_sorted,
+                                                                   const uint32_t* pos_sorted,
+                                                                   const unsigned int* count, int cap) {
+    __shared__ double ebuf[WIDE_ROUND];  // also the pairwise leaf sums
+    __shared__ int lstart[NP_MAX_LEAVES];
+    __shared__ int llen[NP_MAX_LEAVES];
+    __shared__ double sm64[64];
+    __shared__ int smi[16];
+    __shared__ int cut_sh, nleaf_sh;
+    __shared__ double acc_sh;
+    const int b = blockIdx.x;
+    if (!ws[b].active) return;
+    const int tid = threadIdx.x;
+    const ns_stream_state st = p.state[b];
+    const uint64_t* sk = keys_sorted + (int64_t)b * cap;
+    const uint32_t* sp = pos_sorted + (int64_t)b * cap;
+    const int N = (int)count[b];
+    const double* row = (const double*)p.logits + (int64_t)b * p.ld;
+    auto val = [&](int i) -> double { return __longlong_as_double((long long)sk[i]); };  // key 0 -> 0.0
+    auto np_sum = [&](auto&& f) -> double { return block_np_sum(N, f, ebuf, lstart, llen, &nleaf_sh); };
+
+    // P1: crypto policy: p = v / np.sum(v), then (unless isclose(T, 1)) tempered and renormalised
+    const bool crypto = p.rk_crypto != 0;
+    const double Tq = p.rk_ptemp;
+    double tot = 1.0, a0 = 0.0, Q = 1.0;
+    if (crypto) {
+        tot = np_sum([&](int j) -> double { return row[j]; });
+        if (Tq > 0.0) {
+            a0 = log(val(0) / tot + 1e-12) / Tq;
+            Q = np_sum([&](int j) -> double { return exp(log(row[j] / tot + 1e-12) / Tq - a0); });
         }
-        return;
     }
-    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
-    const int32_t tok = p.in_token[b];
-    int found = 0x7FFFFFFF;
-    if (tok >= 0 && tok < p.V) {
-        const uint64_t kt = wkey(Elem<T>::load1(rowc, tok), (uint32_t)tok);
-        for (int i = tid; i < (1 << c); i += WIDE_THREADS)
-            if (sk[i] == kt) found = i;
+    auto pf = [&](int i) -> double {  // rank order
+        if (!crypto) return val(i);
+        const double q = val(i) / tot;
+        return Tq > 0.0 ? exp(log(q + 1e-12) / Tq - a0) / Q : q;
+    };
+    auto pfpos = [&](int j) -> double {  // array position order (the reference's arrays)
+        if (!crypto) return row[j];
+        const double q = row[j] / tot;
+        return Tq > 0.0 ? exp(log(q + 1e-12) / Tq - a0) / Q : q;
+    };
+    // P2: support n = #{p > 0} (a prefix of the ranking), quality cut
+    int fz = N;
+    for (int i = tid; i < N; i += WIDE_THREADS)
+        if (i < fz && !(pf(i) > 0.0)) fz = i;
+    int n = block_min_int(fz, smi);
+    n = rank_quality_cut(p, N, n, pf, ebuf, smi, cut_sh, acc_sh);
+    // P3: apply_quality renormalises the kept values by np.sum over the array (zeros elsewhere); the support is
+    // what stays > 0 (_rank_tokens' mask)
+    const bool filtered = p.rk_top_k > 0 || p.rk_top_p > 0.0 || p.rk_min_prob >= 0.0;
+    double F = 1.0, S_trace = crypto ? tot : 0.0;
+    if ((crypto || filtered) && n > 0) {
+        const uint64_t kth = sk[n - 1];
+        const uint32_t pth = sp[n - 1];
+        auto kept = [&](int j) -> bool {
+            const uint64_t kj = prob_key(row[j]);
+            return kj > kth || (kj == kth && (uint32_t)j <= pth);
+        };
+        F = np_sum([&](int j) -> double { return kept(j) ? pfpos(j) : 0.0; });
+        S_trace = F;
+        if (!(F > 0.0 && F <= 1.7976931348623157e308)) {  // QualityConfigError in the reference: range error
+            n = 0;
+        } else {
+            int fz2 = n;
+            for (int i = tid; i < n; i += WIDE_THREADS)
+                if (i < fz2 && !(pf(i) / F > 0.0)) fz2 = i;
+            n = block_min_int(fz2, smi);
+        }
     }
-    const int idx = block_min_int(found, smi);
-    if (tid != 0) return;
-    if (idx == 0x7FFFFFFF) {
-        p.state[b].flags = st.flags | NS_ST_ERR_DIVERGE | NS_ST_DONE;
-        return;
+    // P4: cap over the array's entries (a dict that went through apply_quality keeps only its positive entries)
+    if (!crypto) {
+        const int U = (p.rk_dict && filtered) ? n : N;
+        n = rank_cap(p, U, n, [&](int i) -> double { return filtered ? pf(i) / F : pf(i); }, sm64, smi);
     }
-    const int keep = min(max(p.rk_keep[b], 0), c);
-    uint8_t* ob = p.out_bits + (int64_t)b * p.out_stride;
-    for (int t = 0; t < keep; ++t) {
-        const int64_t bp = st.bit_pos + t;
-        const uint8_t bitv = (uint8_t)((idx >> (c - 1 - t)) & 1);
-        const uint8_t m = (uint8_t)(0x80u >> (bp & 7));
-        ob[bp >> 3] = bitv ? (uint8_t)(ob[bp >> 3] | m) : (uint8_t)(ob[bp >> 3] & ~m);
-    }
-    ns_stream_state ns = st;
-    ns.bit_pos = st.bit_pos + keep;
-    ns.ntokens = st.ntokens + 1;
-    p.state[b] = ns;
-    if (p.trace) {
-        ns_step_trace tr = {n, c, idx, keep, tok, 0, S};
-        p.trace[b] = tr;
-    }
+    // P5: selection / emission; the token of rank i is the id of its array position
+    auto id_of = [&](int i) -> int32_t {
+        const uint32_t j = sp[i];
+        return p.rk_idmap ? p.rk_idmap[(int64_t)b * p.rk_idmap_stride + j] : (int32_t)j;
+    };
+    rank_emit<DECODE>(p, b, st, n, S_trace, id_of, [&](int i, int32_t tok) -> bool { return id_of(i) == tok; },
+                      smi);
 }
 
 }  // namespace nsg
@@ -2594,6 +2859,16 @@ int nsg_wide_alloc(ns_ctx* ctx) {
     if (rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, w.keys_in, w.keys_out, (unsigned int)n,
                                                 (unsigned int)ctx->max_batch, w.begin, w.end, 0, 49) != hipSuccess)
         return NS_ERR_HIP;
+    if (ctx->dtype == NS_DTYPE_F64) {  // provider rows: 64-bit value keys sorted with their array positions
+        if (hipMalloc((void**)&w.vals_in, n * 4) != hipSuccess || hipMalloc((void**)&w.vals_out, n * 4) != hipSuccess)
+            return NS_ERR_HIP;
+        size_t pbytes = 0;
+        if (rocprim::segmented_radix_sort_pairs_desc(nullptr, pbytes, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
+                                                     (unsigned int)n, (unsigned int)ctx->max_batch, w.begin, w.end,
+                                                     0, 64) != hipSuccess)
+            return NS_ERR_HIP;
+        bytes = bytes > pbytes ? bytes : pbytes;
+    }
     w.sort_tmp_bytes = bytes;
     if (hipMalloc(&w.sort_tmp, bytes ? bytes : 16) != hipSuccess) return NS_ERR_HIP;
     return NS_OK;
@@ -2602,7 +2877,7 @@ int nsg_wide_alloc(ns_ctx* ctx) {
 void nsg_wide_free(ns_ctx* ctx) {
     NsgWide& w = ctx->wide;
     for (void* ptr : {(void*)w.keys_in, (void*)w.keys_out, (void*)w.count, (void*)w.begin, (void*)w.end,
-                      (void*)w.todo, (void*)w.stat, w.sort_tmp})
+                      (void*)w.todo, (void*)w.stat, w.sort_tmp, (void*)w.vals_in, (void*)w.vals_out})
         if (ptr) (void)hipFree(ptr);
     w = NsgWide();
 }
@@ -2656,7 +2931,28 @@ static bool rank_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
     return hipGetLastError() == hipSuccess;
 }
 
+template <bool DECODE>
+static bool rank64_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
+    NsgWide& w = ctx->wide;
+    const int B = p.B;
+    hipLaunchKernelGGL(nsg::rank64_prep_kernel<DECODE>, dim3((B + 255) / 256), dim3(256), 0, s, p, w.stat, w.count);
+    const int nchunk = (p.V + nsg::COLLECT_CHUNK - 1) / nsg::COLLECT_CHUNK;
+    hipLaunchKernelGGL(nsg::rank64_collect_kernel, dim3(nchunk, B), dim3(256), 0, s, p, w.stat, w.keys_in, w.vals_in,
+                       w.count, w.cap);
+    hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
+                       w.count, w.begin, w.end, 0u, nullptr);
+    size_t bytes = w.sort_tmp_bytes;
+    if (rocprim::segmented_radix_sort_pairs_desc(w.sort_tmp, bytes, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
+                                                 (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin, w.end,
+                                                 0, 64, s) != hipSuccess)
+        return false;
+    hipLaunchKernelGGL((nsg::wide_rank64_kernel<DECODE>), dim3(B), dim3(nsg::WIDE_THREADS), 0, s, p, w.stat,
+                       w.keys_out, w.vals_out, w.count, w.cap);
+    return hipGetLastError() == hipSuccess;
+}
+
 bool nsg_rank_launch(ns_ctx* ctx, const nsg::StepParams& p, bool decode, hipStream_t s) {
+    if (ctx->dtype == NS_DTYPE_F64) return decode ? rank64_launch_t<true>(ctx, p, s) : rank64_launch_t<false>(ctx, p, s);
     if (ctx->dtype == NS_DTYPE_F16)
         return decode ? rank_launch_t<_Float16, true>(ctx, p, s) : rank_launch_t<_Float16, false>(ctx, p, s);
     return decode ? rank_launch_t<float, true>(ctx, p, s) : rank_launch_t<float, false>(ctx, p, s);

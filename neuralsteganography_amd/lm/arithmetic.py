@@ -520,11 +520,7 @@ class HipArithmeticLM:
             if bad:
                 redo = [0] * B
                 for b in bad:
-                    ranked = sess.ranked_ids(b)
-                    try:
-                        coder_tok, _ = bpe_repair(enc, lists[b], pos[b], ranked)
-                    except IndexError:  # a merge candidate runs past the end of the text: unrepairable
-                        coder_tok = int(ranked[0])
+                    coder_tok = repair_or_restore(enc, lists[b], pos[b], sess.ranked_ids(b), strict=strict)
                     if any(not 0 <= t < self.vocab for t in lists[b]):
                         raise ConfigurationError(f"repair produced a token id outside [0, {self.vocab})")
                     redo[b] = coder_tok
@@ -650,4 +646,26 @@ def bpe_repair(enc, inp: List[int], i: int, ranked_ids: Sequence[int]):
     return int(ranked_ids[0]), False
 
 
-__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality", "bpe_repair", "stop_candidates"]
+def repair_or_restore(enc, inp: List[int], i: int, ranked_ids: Sequence[int], *, strict: bool) -> int:
+    """:func:`bpe_repair` for the batched decoder: the token the coder decodes at position ``i``.
+
+    The reference's longer-token branch reads ``inp[i + num_extra]`` and deletes ``inp[i + j]`` as it goes; when
+    the merge reaches past the end of the text that raises ``IndexError`` out of ``decode_arithmetic``
+    (``code_base/arithmetic.py:321-333``) -- possibly after ``inp`` was already edited.  Here the list is restored
+    to its state before the attempt (so the LM is fed the received token and later spans are cut from an unedited
+    list); strict decoding raises :class:`DecodeDivergenceError` as the reference raises, the lenient span
+    splitter decodes the rank-0 token as an unrepairable one."""
+    snapshot = list(inp)
+    try:
+        return bpe_repair(enc, inp, i, ranked_ids)[0]
+    except IndexError:
+        inp[:] = snapshot
+        if strict:
+            from ..codec.errors import DecodeDivergenceError
+
+            raise DecodeDivergenceError(f"BPE repair at token {i} runs past the end of the text") from None
+        return int(ranked_ids[0])
+
+
+__all__ = ["HipArithmeticLM", "ByteTokenizer", "coder_params_from_quality", "bpe_repair", "repair_or_restore",
+           "stop_candidates"]

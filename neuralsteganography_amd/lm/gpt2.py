@@ -9,13 +9,14 @@ forward semantics (``code_base/arithmetic.py:12-48,115-122``):
   (``_position_ids_for_cache``, ``:44-48``) and attends to the whole cache: the reference never truncates
   it (``limit_past`` slices head_dim, a no-op, ``code_base/utils.py:19-30``).
 
-Decode steps on the GPU in fp16 (the product configuration) run entirely on hand-written HIP kernels whose
-per-stream results do not depend on the batch size (``include/nsg_lm.h``: MFMA GEMMs with the bias / gelu /
-residual epilogues fused, layer norms, embedding; ``include/nsg_attn.h``: KV append fused with a fixed-split
-online-softmax attention, HBM-bound on the cache), so a cover encoded in a batch of B streams decodes to the
-same logits alone.  The shared-context prefill (identical for encoder and decoder: one stream, T tokens),
-fp32 compute and the CPU keep PyTorch (``addmm`` + ``scaled_dot_product_attention``) as the forward's reference
-configuration (tests pin the two against each other and against Hugging Face).
+In fp16 on the GPU (the product configuration) every forward runs on hand-written HIP kernels whose per-stream
+results do not depend on the batch size (``include/nsg_lm.h``: MFMA GEMMs with the bias / gelu / residual
+epilogues fused, layer norms, embedding; ``include/nsg_attn.h``: the decode step's KV append fused with a
+fixed-split online-softmax attention, HBM-bound on the cache, and a causal MFMA flash attention for whole
+sequences): the decode steps, the shared-context prefill, the guard's scoring forward and the ``max_context``
+window forward.  A cover encoded in a batch of B streams decodes to the same logits alone, and a text scores the
+same alone or in a batch.  fp32 compute and the CPU keep PyTorch (``addmm`` + ``scaled_dot_product_attention``) as
+the forward's reference configuration (tests pin the two against each other and against Hugging Face).
 
 Logits are produced as ``h @ wte^T`` into a ``[B, ld]`` buffer with ``ld = row_stride(V)`` (zero weight
 columns beyond V), so the coder reads 16-byte-aligned rows without a copy.  Weights are taken from a
@@ -132,9 +133,18 @@ class BatchedGPT2:
         s = self.shape
         return 2 * s.n_layer * B * s.n_embd * torch.tensor([], dtype=self.kv_torch_dtype).element_size()
 
-    def fit_positions(self, B: int, want: int, reserve: float = 0.15, count_cached: bool = True) -> int:
-        """Largest cache length <= ``want`` that fits the device's free memory (keeping ``reserve`` of it for
-        activations and logits).  The reference's cache is unbounded; at B = 4096 a 1 KiB payload needs ~1.1k
+    def headroom_bytes(self, B: int) -> int:
+        """Device memory kept free beside the KV cache for what is allocated after it: the logit
+        rows of the step (fixed graph buffer, a coder-side copy, the decoder's), the wide coder path's scratch
+        (two 8-byte key arrays per id), the activation buffers of the native step and the guard's scoring chunk,
+        plus 2 GiB for the runtime and the allocator's rounding."""
+        s = self.shape
+        per_stream = self.ld * 4 * 3 + s.vocab * 16 + 16 * s.n_embd * 2
+        return (2 << 30) + int(B) * per_stream
+
+    def fit_positions(self, B: int, want: int, reserve: float = 0.05, count_cached: bool = True) -> int:
+        """Largest cache length <= ``want`` that fits the device's free memory, minus :meth:`headroom_bytes` and
+        a ``reserve`` fraction.  The reference's cache is unbounded; at B = 4096 a 1 KiB payload needs ~1.1k
         positions (170 GB for GPT-2-small fp16), so the budget is sized from what is free, not guessed."""
         if self.position_cap is not None:
             want = min(int(want), int(self.position_cap))
@@ -150,7 +160,8 @@ class BatchedGPT2:
         free, _ = torch.cuda.mem_get_info(self.device)
         if count_cached:
             free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-        return max(1, min(int(want), int(free * (1.0 - reserve)) // self.kv_bytes_per_position(B)))
+        budget = int(free * (1.0 - reserve)) - self.headroom_bytes(B)
+        return max(1, min(int(want), budget // self.kv_bytes_per_position(B)))
 
     def _native_buffers(self, B: int):
         """Activation buffers of the native decode step (fixed addresses: a captured graph replays them)."""
@@ -287,22 +298,32 @@ class BatchedGPT2:
         if min(ctx) < 0 or max(ctx) >= self.shape.vocab:  # host check: never gather out of the table
             raise ValueError(f"context token ids must lie in [0, {self.shape.vocab})")
         ids = torch.tensor([ctx], device=self.device, dtype=torch.long)
-        pos = torch.arange(T, device=self.device) % self.shape.n_positions
-        h = self.wte[ids] + self.wpe[pos][None]
         if self.native:
-            # the context's K/V are the same for every stream: keep ONE copy (kp/vp), read by every stream's
-            # attention (ns_decode_attention_prefix) -- B-fold less prefix traffic and memory, identical bits
-            self.allocate(1, T, dtype=self.dtype, plain=True)  # the prefill itself runs in fp16 (PyTorch path)
-            for i in range(self.shape.n_layer):
-                h = self._block(i, h, T, causal=True)
-            kp, vp = self.k_cache, self.v_cache  # [n_layer, 1, H, T, D]
+            # the context runs once on the native sequence kernels (MFMA GEMMs + causal MFMA attention, no PyTorch
+            # attention or BLAS), and its K/V -- the same for every stream -- are kept ONCE (kp/vp), read by every
+            # stream's attention (ns_decode_attention_prefix): B-fold less prefix traffic and memory, identical bits
+            s = self.shape
+            H, D, C = s.n_head, s.n_embd // s.n_head, s.n_embd
+            kp = torch.empty((s.n_layer, 1, H, T, D), device=self.device, dtype=self.dtype)
+            vp = torch.empty_like(kp)
+
+            def keep_kv(i, qkv):
+                kp[i, 0] = qkv[:, C:2 * C].view(T, H, D).transpose(0, 1)
+                vp[i, 0] = qkv[:, 2 * C:].view(T, H, D).transpose(0, 1)
+
+            self.k_cache = self.v_cache = None
+            hs = self._seq_native(ids, kv_hook=keep_kv)
+            lg = self._head_native(hs[T - 1:T])
             if self.kv_dtype == "fp8":  # the context rows get the same conversion as the decode-time appends
                 kp, vp = self._quantize_fp8(kp), self._quantize_fp8(vp)
             # the one-stream prefill cache survives as kp/vp: it is not free memory for the stream cache
-            self.k_cache = self.v_cache = None
             self._allocate_fitted(B, T, max_new, T0=T)
             self.kp, self.vp = kp, vp
+            self.L = T
+            return lg.expand(B, -1).contiguous()
         else:
+            pos = torch.arange(T, device=self.device) % self.shape.n_positions
+            h = self.wte[ids] + self.wpe[pos][None]
             self._allocate_fitted(B, 0, T + max_new)
             if self.max_len < T + 1:
                 raise RuntimeError(f"no device memory for a {T + 1}-position KV cache at B={B}")
@@ -319,15 +340,111 @@ class BatchedGPT2:
         lg = self._logits(h[:, -1])
         return lg.expand(B, -1).contiguous()
 
+    def _seq_native(self, ids: torch.Tensor, kv_hook=None) -> torch.Tensor:
+        """Causal forward of B whole sequences ``[B, T]`` (positions 0..T-1, no cache) on the native kernels:
+        embedding + ln_1, then per layer the c_attn GEMM, the causal MFMA attention (``ns_seq_attention``), c_proj
+        with the residual in its epilogue, ln_2, c_fc with gelu_new, c_proj + residual.  Returns the residual
+        stream ``[B*T, C]`` before ln_f.  Every row's result depends on its own sequence only (the GEMMs' and the
+        attention's batch invariance), so a text scores the same alone or in a batch.  ``kv_hook(layer, qkv)``
+        sees each layer's ``[B*T, 3C]`` c_attn output (the prefill keeps the context's K/V)."""
+        from .. import _lib
+        from ..coder import _stream_handle
+
+        s = self.shape
+        B, T = ids.shape
+        C, H = s.n_embd, s.n_head
+        D = C // H
+        M = B * T
+        L = _lib.lib()
+        st = _stream_handle()
+        dev, dt = self.device, self.dtype
+        tok = ids.to(device=dev, dtype=torch.int32).reshape(M).contiguous()
+        h = torch.empty((M, C), device=dev, dtype=dt)
+        a = torch.empty_like(h)
+        o = torch.empty_like(h)
+        qkv = torch.empty((M, 3 * C), device=dev, dtype=dt)
+        f = torch.empty((M, 4 * C), device=dev, dtype=dt)
+        eps = float(s.eps)
+
+        def ok(rc, what):
+            if rc != 0:
+                raise RuntimeError(f"{what} failed ({rc})")
+
+        def gemm(x, wt, bias, y, epi, N, K):
+            ok(L.ns_lm_gemm(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0),
+                            bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), M, N, K, epi,
+                            st), "ns_lm_gemm")
+
+        def ln(x, w, b, y):
+            ok(L.ns_lm_layernorm(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y.data_ptr(), C, M, C, eps, st),
+               "ns_lm_layernorm")
+
+        lw0 = self.layers[0]
+        ok(L.ns_lm_embed_seq_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions, T,
+                                h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(), a.data_ptr(), C, M,
+                                C, eps, st), "ns_lm_embed_seq_ln")
+        for i, lw in enumerate(self.layers):
+            if i > 0:
+                ln(h, lw["ln1_w"], lw["ln1_b"], a)
+            gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
+            if kv_hook is not None:
+                kv_hook(i, qkv)
+            ok(L.ns_seq_attention(qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), B, T, H, D,
+                                  1.0 / math.sqrt(D), st), "ns_seq_attention")
+            gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
+            ln(h, lw["ln2_w"], lw["ln2_b"], a)
+            gemm(a, lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C, C)
+            gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
+        return h
+
+    def _head_native(self, hrows: torch.Tensor) -> torch.Tensor:
+        """ln_f + the head GEMM of ``[R, C]`` residual rows on the native kernels: ``[R, ld]`` logits."""
+        from .. import _lib
+        from ..coder import _stream_handle
+
+        L = _lib.lib()
+        st = _stream_handle()
+        C = self.shape.n_embd
+        hrows = hrows.contiguous()
+        R = hrows.shape[0]
+        a = torch.empty_like(hrows)
+        rc = L.ns_lm_layernorm(hrows.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, R,
+                               C, float(self.shape.eps), st)
+        if rc != 0:
+            raise RuntimeError(f"ns_lm_layernorm failed ({rc})")
+        out = torch.empty((R, self.ld), device=self.device, dtype=self.logits_dtype)
+        epi = _lib.NS_LM_EPI_STORE_F32 if out.dtype == torch.float32 else _lib.NS_LM_EPI_STORE
+        rc = L.ns_lm_gemm(a.data_ptr(), C, self.head_t.data_ptr(), self.head_t.stride(0), None, out.data_ptr(),
+                          out.stride(0), R, self.ld, C, epi, st)
+        if rc != 0:
+            raise RuntimeError(f"ns_lm_gemm failed ({rc})")
+        return out
+
+    @torch.no_grad()
+    def window_logits(self, ids: torch.Tensor) -> torch.Tensor:
+        """Next-token logits ``[B, ld]`` of B token windows ``[B, W]`` each run from scratch with positions
+        0..W-1 -- the src provider's ``_ModelAdapter`` forward over a context trimmed to ``max_context``
+        (``src/neuralstego/lm/arithmetic.py:45-74``)."""
+        B, W = ids.shape
+        if W > self.shape.n_positions:
+            raise ValueError(f"window longer than n_positions ({self.shape.n_positions})")
+        if self.native:
+            hs = self._seq_native(ids)
+            return self._head_native(hs.view(B, W, -1)[:, -1])
+        return self.forward_sequences(ids)[:, -1].contiguous()
+
     @torch.no_grad()
     def forward_sequences(self, ids: torch.Tensor) -> torch.Tensor:
         """Causal forward of B right-padded sequences ``[B, T]`` with positions ``0..T-1`` and no cache (the
         guard's scoring pass, ``metrics/lm_scorer.py:121-131``); returns ``[B, T, ld]`` logits in
-        ``logits_dtype``.  Padding only follows the real tokens, so causality keeps it out of their rows."""
+        ``logits_dtype``.  Padding only follows the real tokens, so causality keeps it out of their rows.  fp16 on
+        the GPU runs the native sequence kernels (a text's scores do not depend on the batch it is scored in)."""
         s = self.shape
         B, T = ids.shape
         if T > s.n_positions:
             raise ValueError(f"sequence longer than n_positions ({s.n_positions})")
+        if self.native:
+            return self._head_native(self._seq_native(ids)).view(B, T, self.ld)
         H, C = s.n_head, s.n_embd
         D = C // H
         pos = torch.arange(T, device=self.device)
@@ -465,7 +582,8 @@ def random_gpt2(name: str = "gpt2", *, seed: int = 1234, **overrides):
              "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),
              # HooshvareLab/gpt2-fa (config C4): GPT-2-small geometry with its 42,001-id Persian vocabulary
              # (unverified offline -- architecture only, random weights)
-             "gpt2-fa": dict(n_layer=12, n_head=12, n_embd=768, vocab_size=42001),
+             "gpt2-fa": dict(n_layer=12, n_head=12, n_embd=768, vocab_size=42001, bos_token_id=42000,
+                             eos_token_id=42000),
              "tiny": dict(n_layer=2, n_head=2, n_embd=64)}
     kw = dict(sizes[name])
     kw.update(overrides)

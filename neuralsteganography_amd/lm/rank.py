@@ -8,9 +8,11 @@ pops one and needs it (the rank coder cannot decode without the history, ``codec
 Quality keys follow ``lm/arithmetic.py:77-112``: temp / temperature, topk / top_k, top_p, min_prob,
 cap_per_token_bits, max_context.
 
-Deviation: the reference re-runs the whole (trimmed) context per token; this provider keeps a KV cache with
-positions modulo ``n_positions`` -- identical logits while the context fits ``n_positions`` (and no
-``max_context`` trimming is requested), which covers the api's packet-sized streams.
+Without ``max_context`` the reference re-runs the whole context per token; this provider keeps a KV cache with
+positions modulo ``n_positions`` -- the same logits while the context fits ``n_positions`` (the reference's forward
+fails beyond it).  With ``max_context`` (``lm/arithmetic.py:50-51,106-112``) the trimmed window's positions shift
+every token, so no cache applies: each step re-runs every stream's last ``max_context`` tokens from scratch
+(:class:`WindowedLM`, the batched GPT-2's native causal sequence forward), exactly the reference's computation.
 """
 
 from __future__ import annotations
@@ -48,6 +50,60 @@ def _temperature(quality: Optional[Mapping[str, object]]) -> float:
     return 1.0
 
 
+def _max_context(quality: Optional[Mapping[str, object]]) -> Optional[int]:
+    """``_quality_max_context`` (``lm/arithmetic.py:106-112``)."""
+    if not quality:
+        return None
+    for key in ("max_context", "maxContext"):
+        if key in quality and quality[key] is not None:
+            return int(quality[key])
+    return None
+
+
+class WindowedLM:
+    """``prefill`` / ``step`` of a batched GPT-2 where every query re-runs the stream's context trimmed to its last
+    ``window`` ids from scratch (positions 0..W-1): ``_ModelAdapter.next_token_probs`` with ``max_context``
+    (``src/neuralstego/lm/arithmetic.py:45-74``), which ``encode_with_lm`` also trims to (``codec/arithmetic.py:
+    337-347``).  One batched causal forward of ``[B, W]`` tokens per step (``BatchedGPT2.window_logits``)."""
+
+    takes_full_context = True  # the whole context reaches prefill (trimmed here, as the reference trims it)
+
+    def __init__(self, lm, window: int):
+        import torch
+
+        if window <= 0:
+            raise ConfigurationError("max_context must be positive")
+        if not hasattr(lm, "window_logits"):
+            raise ConfigurationError("max_context needs a GPT-2 provider (BatchedGPT2.window_logits)")
+        if window > lm.shape.n_positions:
+            raise ConfigurationError(f"max_context {window} exceeds the model's {lm.shape.n_positions} positions")
+        self.lm, self.window, self.shape = lm, int(window), lm.shape
+        self.device = lm.device
+        self.ids = torch.zeros((0, 0), dtype=torch.long)
+
+    def _logits(self):
+        return self.lm.window_logits(self.ids[:, -self.window:].contiguous())
+
+    def prefill(self, context, B: int, max_new: int):
+        import torch
+
+        del max_new
+        ctx = [int(t) for t in context]
+        if not ctx:
+            raise ConfigurationError("context must contain at least one token")  # lm/arithmetic.py:46-48
+        if min(ctx) < 0 or max(ctx) >= self.shape.vocab:
+            raise ConfigurationError(f"context token ids must lie in [0, {self.shape.vocab})")
+        self.ids = torch.tensor(ctx[-self.window:], device=self.device, dtype=torch.long)[None].repeat(int(B), 1)
+        return self._logits()
+
+    def step(self, tokens):
+        import torch
+
+        tok = tokens.to(device=self.device, dtype=torch.long).view(-1, 1)
+        self.ids = torch.cat([self.ids[:, -(self.window - 1):] if self.window > 1 else self.ids[:, :0], tok], 1)
+        return self._logits()
+
+
 class HipRankLM:
     """Rank-coder provider: batched GPT-2 (or any ``prefill``/``step`` batched LM) + the HIP rank kernel."""
 
@@ -65,6 +121,8 @@ class HipRankLM:
             dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
             ldt = torch.float16 if logits_dtype == "f16" else torch.float32
             batched_lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt)
+        if getattr(batched_lm, "prob_rows", False):
+            logits_dtype = "f64"  # a generic provider's own float64 ProbDists (ProviderBatchedLM)
         self.lm = batched_lm
         self.vocab = self.lm.shape.vocab
         # the byte stand-in only where it can spell bytes (a small provider vocabulary has no tokenizer: its
@@ -79,19 +137,27 @@ class HipRankLM:
         self._encode_states: List[CodecState] = []
         self._decode_states: Deque[CodecState] = deque()
 
-    def _coder(self, B: int) -> CoderContext:
-        """One coder context (the parameters never change here) sized for the largest batch seen so far: a
-        smaller batch reuses it, a larger one replaces it (the kernels take B per call)."""
+    def _coder(self, B: int, vocab: Optional[int] = None) -> CoderContext:
+        """One coder context (the parameters never change here) sized for the largest batch -- and, for a
+        generic provider's rows, the longest row -- seen so far: a smaller one reuses it, a larger one replaces it
+        (the kernels take B per call; a provider row's entry count is registered per step)."""
+        V = max(int(vocab or 0), self.vocab)
         ctx = self._ctx.get(0)
-        if ctx is not None and ctx.max_batch < B:
+        if ctx is not None and (ctx.max_batch < B or ctx.params.vocab < V):
             ctx.close()
             ctx = None
         if ctx is None:
-            params = CoderParams(vocab=self.vocab, precision=16, temp=1.0, topk=self.vocab, dtype=self.logits_dtype,
-                                 banned=[])
+            params = CoderParams(vocab=V, precision=16, temp=1.0, topk=V, dtype=self.logits_dtype, banned=[])
             ctx = CoderContext(params, max_batch=max(B, 1), device=self.device_index)
             self._ctx[0] = ctx
+        self.vocab = V
         return ctx
+
+    def _fit(self, sess, rows):
+        """A provider step whose rows outgrow the context (a longer dict, a larger ndarray) moves the session to a
+        wider context: its stream state lives in the session's tensors, the context holds scratch only."""
+        if getattr(rows, "prob_rows", False) and rows.ncols > sess.ctx.params.vocab:
+            sess.ctx = self._coder(sess.B, rows.ncols)
 
     # ------------------------------------------------------------------ protocol (api.py:42-56)
     def encode_seed(self, text: str) -> List[int]:
@@ -130,12 +196,20 @@ class HipRankLM:
         self._decode_states = deque(dict(s) for s in states)
 
     # ------------------------------------------------------------------ batched
-    def _context(self, context: Sequence[int]) -> List[int]:
+    def _context(self, context: Sequence[int], lm=None) -> List[int]:
         """The prefill context: GPT-2 keeps the reference's last 1022 ids (and needs one); a host provider
-        (``ProviderBatchedLM``) gets it untrimmed, as ``next_token_probs`` would."""
-        if getattr(self.lm, "takes_full_context", False):
+        (``ProviderBatchedLM``) or a ``max_context`` window gets it untrimmed, as ``next_token_probs`` would."""
+        if getattr(lm if lm is not None else self.lm, "takes_full_context", False):
             return [int(t) for t in context]
         return list(context)[-1022:] or [0]
+
+    def _lm_for(self, quality):
+        """The batched LM of a call: the provider's own, or a :class:`WindowedLM` over it when the quality asks for
+        ``max_context`` (a generic provider's context window is applied by ``codec.rank`` instead)."""
+        mc = _max_context(quality)
+        if mc is None or getattr(self.lm, "prob_rows", False):
+            return self.lm
+        return WindowedLM(self.lm, mc)
 
     def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], max_steps: int = 1 << 16) -> List[List[int]]:
@@ -162,15 +236,25 @@ class HipRankLM:
             sess.nbits[[i for i, e in enumerate(empty) if e]] = 0
         import torch
 
-        logits = self.lm.prefill(self._context(context), B, 8 * max(len(p) for p in payloads) + 2)
-        every = 1 if getattr(self.lm, "takes_full_context", False) else 8  # host providers: no wasted queries
+        lm = self._lm_for(quality)
+        logits = lm.prefill(self._context(context, lm), B, 8 * max(len(p) for p in payloads) + 2)
+        self._fit(sess, logits)
+        # host providers (ProviderBatchedLM): check after every step, so the provider is never queried past the
+        # last token (the reference's loop ends before another next_token_probs call, codec/arithmetic.py:146)
+        host = getattr(lm, "prob_rows", False)
+        every = 1 if host else 8
         for t in range(max_steps):
             if t % every == 0:
                 sess.raise_errors()
                 if sess.all_done():
                     break
+            self._fit(sess, logits)
             tok = sess.step(logits)
-            logits = self.lm.step(tok.to(torch.long))
+            if host:
+                sess.raise_errors()
+                if sess.all_done():
+                    break
+            logits = lm.step(tok.to(torch.long))
         toks, cons = sess.tokens(), sess.consumed()
         states = []
         for i in range(B):
@@ -189,18 +273,21 @@ class HipRankLM:
         if states is None:
             states = [self._decode_states.popleft() if self._decode_states else {} for _ in range(B)]
         hist = [list(s.get("history") or ()) for s in states]
-        for tl in token_lists:
-            if any(not 0 <= int(t) < self.vocab for t in tl):
-                from ..codec.errors import DecodeDivergenceError
+        if not getattr(self.lm, "prob_rows", False):  # GPT-2 ids feed the embedding gather: check on the host
+            for tl in token_lists:
+                if any(not 0 <= int(t) < self.vocab for t in tl):
+                    from ..codec.errors import DecodeDivergenceError
 
-                raise DecodeDivergenceError(f"token id outside [0, {self.vocab})")
+                    raise DecodeDivergenceError(f"token id outside [0, {self.vocab})")
         ctx = self._coder(B)
         sess = RankDecodeSession(ctx, token_lists, hist, temp=_temperature(quality), quality=quality)
-        logits = self.lm.prefill(self._context(context), B, max(sess.T, 1) + 1)
+        lm = self._lm_for(quality)
+        logits = lm.prefill(self._context(context, lm), B, max(sess.T, 1) + 1)
         for t in range(sess.T):
+            self._fit(sess, logits)
             sess.step(logits)
             if t + 1 < sess.T:
-                logits = self.lm.step(sess.tok[t].to(torch.long))
+                logits = lm.step(sess.tok[t].to(torch.long))
         out = []
         for i, pl in enumerate(sess.payloads()):
             nb = states[i].get("residual_bits")

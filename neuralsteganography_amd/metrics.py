@@ -149,11 +149,13 @@ class HipLMScorer:
                                  nll.data_ptr(), ent.data_ptr(), _stream_handle())
             if rc != 0:
                 raise RuntimeError(f"ns_score_rows failed ({rc})")
-            mask = (lab >= 0).view(len(group), T).double()
-            sn = (nll.view(len(group), T) * mask).sum(1).cpu().numpy()
-            se = (ent.view(len(group), T) * mask).sum(1).cpu().numpy()
+            # per text, its own len - 1 positions summed on the host (numpy's order depends on that count only):
+            # the metrics of a text do not depend on the padded length of the batch it was scored in
+            nh = nll.view(len(group), T).cpu().numpy()
+            eh = ent.view(len(group), T).cpu().numpy()
             for r, g in enumerate(group):
-                out[g] = (float(sn[r]), float(se[r]), len(seqs[g]))
+                n = max(len(seqs[g]) - 1, 0)
+                out[g] = (float(nh[r, :n].sum()), float(eh[r, :n].sum()), len(seqs[g]))
             del logits, rows
             i = j
         return out

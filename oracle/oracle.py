@@ -96,6 +96,12 @@ def lib() -> ctypes.CDLL:
         L.or_rank_step.argtypes = [fp, ctypes.c_int, ctypes.c_double, ctypes.POINTER(OrRankQuality), ctypes.c_int,
                                    u8p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(OrState),
                                    i32p, i32p, u8p, i32p]
+        L.or_np_sum.restype = ctypes.c_double
+        L.or_np_sum.argtypes = [dp, ctypes.c_int64]
+        L.or_rank_step64.restype = ctypes.c_int
+        L.or_rank_step64.argtypes = [dp, ctypes.c_int, i32p, ctypes.c_int, ctypes.POINTER(OrRankQuality), ctypes.c_int,
+                                     u8p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(OrState),
+                                     i32p, i32p, u8p, i32p]
         L.or_encode_batch.restype = ctypes.c_int
         L.or_encode_batch.argtypes = [fp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, i32p, ctypes.c_int,
                                       ctypes.c_double, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int64,
@@ -314,6 +320,73 @@ def rank_decode_stream(row_fn: RowFn, tokens: Sequence[int], consumed: Sequence[
                                 int(consumed[t]), ctypes.byref(st), None, None, _u8(out), ctypes.byref(cap))
         if rc != OR_OK:
             raise RuntimeError(f"oracle rank decode step {t} failed rc={rc}")
+    return out.tobytes()[: nbits // 8]
+
+
+def np_sum(a: np.ndarray) -> float:
+    """numpy's float64 ``sum`` restated (or_np_sum): 8192-element chunks of pairwise sums, left to right."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return lib().or_np_sum(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size)
+
+
+def dist_arrays(dist):
+    """A ProbDist as ``_dist_to_arrays`` sees it (codec/arithmetic.py:388-398): (float64 values, int32 ids or
+    None for an ndarray, dict flag)."""
+    if isinstance(dist, dict):
+        items = sorted(dist.items())
+        return (np.array([float(p) for _, p in items], dtype=np.float64),
+                np.array([int(t) for t, _ in items], dtype=np.int32), True)
+    return np.ascontiguousarray(np.asarray(dist, dtype=np.float64).reshape(-1)), None, False
+
+
+def _rank_step64(dist, rq, mode, pl, nbits, tok, keep, st, out_bits):
+    v, ids, is_dict = dist_arrays(dist)
+    otok, c, cap = ctypes.c_int32(-1), ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = lib().or_rank_step64(v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size,
+                              _i32(ids) if ids is not None else None, int(is_dict), ctypes.byref(rq), mode,
+                              _u8(pl) if pl is not None else None, nbits, tok, keep, ctypes.byref(st),
+                              ctypes.byref(otok), ctypes.byref(c), _u8(out_bits) if out_bits is not None else None,
+                              ctypes.byref(cap))
+    return rc, otok.value, c.value
+
+
+def _trim(ctx, window):
+    return tuple(ctx[-window:]) if window is not None and len(ctx) > window else tuple(ctx)
+
+
+def provider_encode_stream(provider, payload: bytes, *, context=(), quality=None, max_context=None):
+    """``encode_with_lm`` over a ``next_token_probs`` provider (codec/arithmetic.py:122-169): each step queries
+    the provider with the context trimmed to ``max_context`` (``_next_distribution``, :337-348) and ranks its
+    float64 ProbDist with or_rank_step64.  Returns (tokens, bits consumed per token)."""
+    pl = np.frombuffer(bytes(payload), dtype=np.uint8).copy() if payload else np.zeros(1, np.uint8)
+    nbits = 8 * len(payload)
+    rq = rank_quality(quality)
+    st = new_state(1)
+    ctx = [int(t) for t in context]
+    toks, cons = [], []
+    while st.bit_pos < nbits:
+        rc, tok, c = _rank_step64(provider.next_token_probs(_trim(ctx, max_context)), rq, 0, pl, nbits, -1, 0, st,
+                                  None)
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle provider encode step {len(toks)} failed rc={rc}")
+        toks.append(tok)
+        cons.append(c)
+        ctx.append(tok)
+    return toks, cons
+
+
+def provider_decode_stream(provider, tokens, consumed, nbits: int, *, context=(), quality=None, max_context=None):
+    """``decode_with_lm`` over a provider (codec/arithmetic.py:172-231) given the consumption history."""
+    rq = rank_quality(quality)
+    st = new_state(1)
+    out = np.zeros(max(1, (sum(consumed) + 7) // 8 + 8), dtype=np.uint8)
+    ctx = [int(t) for t in context]
+    for t, tok in enumerate(tokens):
+        rc, _, _ = _rank_step64(provider.next_token_probs(_trim(ctx, max_context)), rq, 1, None, 0, int(tok),
+                                int(consumed[t]), st, out)
+        if rc != OR_OK:
+            raise RuntimeError(f"oracle provider decode step {t} failed rc={rc}")
+        ctx.append(int(tok))
     return out.tobytes()[: nbits // 8]
 
 

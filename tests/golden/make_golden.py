@@ -285,6 +285,24 @@ PROVIDER_CONFIGS = {
                                        nbytes=[20]),
     "z3_ctxdict_v500_minp_w6": dict(provider="ctxdict", vocab=500, quality={"min_prob": 1e-3}, max_context=6,
                                     nbytes=[12, 5]),
+    # round 4: float64 rows with near-tied neighbours (1e-9 .. 1e-8 relative), unnormalised,
+    # over GPT-2's 50,257 ids: top_p (binding) + min_prob, min_prob (binding) + top_k; and a dict provider whose
+    # ids exceed 2^17 with top_k + top_p
+    "z4_neartie_v50257_p09_minp": dict(provider="neartie", vocab=50257, scale=0.79,
+                                       quality={"top_p": 0.9, "min_prob": 2e-6}, nbytes=[24, 9]),
+    "z5_neartiedict_v200000_k2000_p095": dict(provider="neartiedict", vocab=200000,
+                                              quality={"top_k": 2000, "top_p": 0.95}, nbytes=[20, 7]),
+    "z6_neartie_v50257_minp_k30000": dict(provider="neartie", vocab=50257, scale=0.79,
+                                          quality={"min_prob": 1.3e-5, "top_k": 30000}, nbytes=[20]),
+}
+
+# crypto.encode_arithmetic / decode_arithmetic over GENERIC providers (the _QualityControlledLM normalises the
+# provider's row with numpy's sum, then tempers / filters): T = 1 with top_p (exact), T = 0.8 with top_k
+CRYPTO_PROVIDER_CONFIGS = {
+    "x1_neartie_v50257_p09": dict(provider="neartie", vocab=50257, scale=0.79, quality={"top_p": 0.9},
+                                  nbytes=[24, 6]),
+    "x2_neartiedict_v200000_t08_k500": dict(provider="neartiedict", vocab=200000,
+                                            quality={"temperature": 0.8, "top_k": 500}, nbytes=[18]),
 }
 
 
@@ -294,9 +312,13 @@ def make_provider(cfg):
         from neuralstego.codec.distribution import MockLM  # src/neuralstego/codec/distribution.py:17-37
 
         return MockLM(vocab_size=cfg["vocab"], alpha=cfg["alpha"])
-    from tests.golden.providers import ContextDictLM
+    from tests.golden import providers
 
-    return ContextDictLM(cfg["vocab"])
+    if cfg["provider"] == "neartie":
+        return providers.NearTieLM(cfg["vocab"], scale=cfg["scale"])
+    if cfg["provider"] == "neartiedict":
+        return providers.NearTieDictLM(cfg["vocab"])
+    return providers.ContextDictLM(cfg["vocab"])
 
 
 def run_provider_config(name, cfg):
@@ -368,6 +390,28 @@ def run_crypto_config(name, cfg):
     return out
 
 
+def run_crypto_provider_config(name, cfg):
+    sys.path.insert(0, str(REF / "src"))
+    from neuralstego.crypto import arithmetic as crypto_coder  # src/neuralstego/crypto/arithmetic.py
+
+    assert Path(crypto_coder.__file__).resolve() == (REF / "src/neuralstego/crypto/arithmetic.py").resolve()
+    out = {"tokens": [], "tok_off": [0], "cons": [], "payload": [], "pay_off": [0], "decoded": [], "dec_off": [0]}
+    for s, nbytes in enumerate(cfg["nbytes"]):
+        payload = synthetic.payload_bytes(s, nbytes)
+        toks, state = crypto_coder.encode_arithmetic(payload, make_provider(cfg), quality=cfg["quality"],
+                                                     seed_text=synthetic.DEFAULT_CONTEXT)
+        dec = crypto_coder.decode_arithmetic(toks, make_provider(cfg), quality=cfg["quality"],
+                                             seed_text=synthetic.DEFAULT_CONTEXT, state=dict(state))
+        assert dec == payload, f"{name} stream {s}: reference round trip failed"
+        out["tokens"] += list(toks); out["tok_off"].append(len(out["tokens"]))
+        out["cons"] += list(state["history"])
+        out["payload"] += list(payload); out["pay_off"].append(len(out["payload"]))
+        out["decoded"] += list(dec); out["dec_off"].append(len(out["decoded"]))
+        print(f"  {name} s={s} bytes={nbytes} tokens={len(toks)} bits/token={8 * nbytes / max(1, len(toks)):.2f}",
+              flush=True)
+    return out
+
+
 def run_compat_config(name, cfg, ref, stable_sort_mode):
     from tests.golden.toy_tokenizer import ToyTokenizer
 
@@ -418,6 +462,22 @@ def main(names=None):
             consumed=np.asarray(res["cons"], dtype=np.int32),
             payload=np.asarray(res["payload"], dtype=np.uint8), pay_off=np.asarray(res["pay_off"], np.int64),
             decoded=np.asarray(res["decoded"], dtype=np.uint8), dec_off=np.asarray(res["dec_off"], np.int64))
+    for name, cfg in CRYPTO_PROVIDER_CONFIGS.items():
+        if names and name not in names:
+            continue
+        res = run_crypto_provider_config(name, cfg)
+        meta = dict(cfg, name=name, kind="crypto_provider", crypto_quality=cfg["quality"],
+                    quality=crypto_rank_quality(cfg["quality"]), payload_seed=synthetic.PAYLOAD_SEED,
+                    context=synthetic.DEFAULT_CONTEXT,
+                    reference="src/neuralstego/crypto/arithmetic.py encode_arithmetic / decode_arithmetic over "
+                              "tests/golden/providers.py " + cfg["provider"])
+        np.savez_compressed(
+            HERE / f"{name}.npz",
+            meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+            tokens=np.asarray(res["tokens"], dtype=np.int32), tok_off=np.asarray(res["tok_off"], np.int64),
+            consumed=np.asarray(res["cons"], dtype=np.int32),
+            payload=np.asarray(res["payload"], dtype=np.uint8), pay_off=np.asarray(res["pay_off"], np.int64),
+            decoded=np.asarray(res["decoded"], dtype=np.uint8), dec_off=np.asarray(res["dec_off"], np.int64))
     for name, cfg in PROVIDER_CONFIGS.items():
         if names and name not in names:
             continue
@@ -426,7 +486,9 @@ def main(names=None):
                     context=synthetic.DEFAULT_CONTEXT,
                     reference="src/neuralstego/codec/arithmetic.py encode_with_lm / decode_with_lm over "
                               + ("codec/distribution.py MockLM" if cfg["provider"] == "mock"
-                                 else "tests/golden/providers.py ContextDictLM"))
+                                 else "tests/golden/providers.py " + {"ctxdict": "ContextDictLM",
+                                                                      "neartie": "NearTieLM",
+                                                                      "neartiedict": "NearTieDictLM"}[cfg["provider"]]))
         np.savez_compressed(
             HERE / f"{name}.npz",
             meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),

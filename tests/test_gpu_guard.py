@@ -237,3 +237,23 @@ def test_cover_text_reveal_with_bpe_repair():
     assert sum(differs) >= 3, "too few covers re-tokenise differently: pick another seed"
     got = cover_reveal_batch(texts, seed_text=seed, quality=q, ecc="none", lm=lm)
     assert got == secrets
+
+
+def test_guard_metrics_are_batch_invariant_1024():
+    """a cover's guard metrics (GPU perplexity / average entropy through the native scoring forward)
+    are bit-identical scored alone and inside a batch of 1,024 texts of other lengths (the reference scores one
+    cover at a time; a cover near the gate threshold must not pass or fail by batch composition)."""
+    from neuralsteganography_amd.lm.arithmetic import ByteTokenizer
+    from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+    from neuralsteganography_amd.metrics import HipLMScorer
+
+    m = random_gpt2("gpt2", seed=22)
+    lm = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16, logits_dtype=torch.float16)
+    sc = HipLMScorer(lm, ByteTokenizer(50257), rows_per_batch=40000)
+    rng = np.random.default_rng(4)
+    words = ["alpha", "beta", "gamma", "delta", "stego", "cover", "token", "text", "x"]
+    texts = [" ".join(rng.choice(words, size=int(rng.integers(1, 40)))) for _ in range(1024)]
+    batch = sc.metrics_batch(texts)
+    for i in (0, 1, 511, 1023):
+        alone = sc.metrics_batch([texts[i]])[0]
+        assert alone == batch[i], i

@@ -529,3 +529,79 @@ def test_window_cover_batch_reveals_alone():
                                  chunk_bytes=24)
     for text, secret in zip(texts, secrets):
         assert cover_reveal(text, seed_text=seed, quality=q, ecc="none", lm=lm) == secret
+
+
+def _seq_attn(qkv, B, T, H, D=64):
+    o = torch.empty((B * T, H * D), device="cuda", dtype=torch.float16)
+    rc = _lib.lib().ns_seq_attention(qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), B, T, H, D, D ** -0.5,
+                                     _stream_handle())
+    assert rc == 0
+    return o
+
+
+@pytest.mark.parametrize("B,T,H", [(1, 1, 12), (3, 5, 12), (2, 64, 4), (2, 100, 12), (1, 300, 16), (2, 1024, 2)])
+def test_seq_attention_matches_fp32_reference(B, T, H):
+    """Causal MFMA flash attention over whole sequences (prefill, guard scoring, max_context windows) vs a plain
+    fp32 PyTorch softmax(q k^T / sqrt(D) + causal mask) v of the same fp16 inputs (P is rounded to fp16 for the
+    PV product: 2e-3 absolute on unit-scale values)."""
+    D = 64
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + T)
+    qkv = torch.randn((B * T, 3 * H * D), generator=g, device="cuda").half()
+    o = _seq_attn(qkv, B, T, H)
+    x = qkv.float().view(B, T, 3, H, D)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    s = s.masked_fill(torch.triu(torch.ones(T, T, device="cuda", dtype=torch.bool), 1), float("-inf"))
+    ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * T, H * D)
+    assert (o.float() - ref).abs().max().item() < 2e-3
+
+
+def test_seq_attention_rows_depend_on_their_sequence_only():
+    """Batch and length invariance of the sequence attention: a sequence's output rows are bit-identical run
+    alone, inside a batch of 5, and right-padded to a longer T (causality keeps padding out of real rows)."""
+    H, D = 12, 64
+    g = torch.Generator(device="cuda").manual_seed(3)
+    T = 150
+    seqs = torch.randn((5, T, 3 * H * D), generator=g, device="cuda").half()
+    big = _seq_attn(seqs.reshape(5 * T, -1).contiguous(), 5, T, H).view(5, T, -1)
+    for b in (0, 4):
+        alone = _seq_attn(seqs[b].contiguous(), 1, T, H)
+        assert torch.equal(alone, big[b])
+        pad = torch.cat([seqs[b], torch.randn((70, 3 * H * D), generator=g, device="cuda").half()]).contiguous()
+        padded = _seq_attn(pad, 1, T + 70, H)
+        assert torch.equal(padded[:T], big[b])
+
+
+def test_native_prefill_and_scoring_use_no_torch_attention_or_blas(monkeypatch):
+    """in fp16 on the GPU the context prefill, the scoring forward and the max_context window
+    forward run on the library's own kernels -- PyTorch's SDPA (AOTriton attn_fwd) and addmm / matmul (hipBLASLt)
+    are never called -- and their logits match Hugging Face's fp32 forward within fp16 tolerance."""
+    import torch.nn.functional as F
+
+    from neuralsteganography_amd.lm.gpt2 import BatchedGPT2, random_gpt2
+
+    m = random_gpt2("gpt2", seed=14)
+    lm = BatchedGPT2(m, device="cuda", compute_dtype=torch.float16, logits_dtype=torch.float32)
+
+    def banned(*a, **k):
+        raise AssertionError("PyTorch attention / BLAS called on the native path")
+
+    monkeypatch.setattr(F, "scaled_dot_product_attention", banned)
+    monkeypatch.setattr(torch, "addmm", banned)
+    monkeypatch.setattr(torch, "matmul", banned)
+    ctx = list(synthetic.DEFAULT_CONTEXT)
+    lg = lm.prefill(ctx, 3, 8)
+    seqs = torch.tensor([ctx, ctx[::-1]], device="cuda")
+    fs = lm.forward_sequences(seqs)
+    wl = lm.window_logits(seqs[:, -9:].contiguous())
+    monkeypatch.undo()
+    with torch.no_grad():
+        ref = m(torch.tensor([ctx])).logits[0].double()
+        ref_rev = m(torch.tensor([ctx[::-1]])).logits[0].double()
+        ref_w = m(torch.tensor([ctx[-9:]])).logits[0, -1].double()
+    V = 50257
+    assert (lg[:, :V].double().cpu() - ref[-1]).abs().max() < 3e-2
+    assert torch.equal(lg[0], lg[2])
+    assert (fs[0, :, :V].double().cpu() - ref).abs().max() < 3e-2
+    assert (fs[1, :, :V].double().cpu() - ref_rev).abs().max() < 3e-2
+    assert (wl[0, :V].double().cpu() - ref_w).abs().max() < 3e-2

@@ -8,6 +8,7 @@ kernels, hipGraph-replayed token loop, HIP coder) at the stated sizes:
   every stream's payload recovered bit for bit; a sample of streams is re-run alone on the eager loop with every
   step's logits captured, which must give the same tokens (the decode step is batch-invariant) and which the
   CPU oracle (``oracle/nsg_oracle.c``, pinned by the reference's own outputs) replays token for token.
+* C4: the same at the gpt2-fa geometry (V = 42,001): one GPU's 4,096-stream share of C4's 32,768.
 * C2: GPT-2-small, B = 1, 1 KiB: every step's logits captured, oracle replay of the whole stream, graph-replayed
   loop equal to the eager loop, decode round trip.
 * C5-like: GPT-2-medium fp16, topk 100, temp 0.9, finish_sent, quality guard ON (the api's default guard, the
@@ -65,34 +66,50 @@ def _free_cache(lm):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.timeout(900)
-def test_c3_gpt2_small_b4096_1kib_roundtrip_bit_exact():
+def _b4096_roundtrip(name, label):
+    """B = 4096 streams x 1 KiB encoded on the hipGraph-replayed product loop, decoded, every payload recovered;
+    three streams re-run alone (eager, logits captured) must give the same tokens, which the oracle replays."""
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
     B, nbytes = 4096, 1024
-    m = random_gpt2("gpt2", seed=1234)
+    m = random_gpt2(name, seed=1234)
     lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=B)
     ctx = synthetic.DEFAULT_CONTEXT
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in range(B)]
     t0 = time.perf_counter()
     toks = lm.encode_batch(bits, ctx, quality=Q_C3)
     t1 = time.perf_counter()
-    print(f"C3 encode done: {t1 - t0:.1f} s", flush=True)
+    print(f"{label} encode done: {t1 - t0:.1f} s", flush=True)
     _free_cache(lm)
     out = lm.decode_batch(toks, ctx, quality=Q_C3)
     t2 = time.perf_counter()
     bad = [s for s in range(B) if out[s][: len(bits[s])] != bits[s]]
-    assert not bad, f"{len(bad)} of {B} streams did not round-trip (first: {bad[:8]})"
+    assert not bad, f"{label}: {len(bad)} of {B} streams did not round-trip (first: {bad[:8]})"
     ntok = sum(map(len, toks))
-    print(f"C3 round trip: {B} x {nbytes} B, {ntok} tokens, encode {t1 - t0:.1f} s, decode {t2 - t1:.1f} s")
+    print(f"{label} round trip: V={lm.vocab}, {B} x {nbytes} B, {ntok} tokens, encode {t1 - t0:.1f} s, "
+          f"decode {t2 - t1:.1f} s", flush=True)
     _free_cache(lm)
     # oracle replay: a sample of streams alone, eager, logits captured (batch-invariant step => same logits)
     sample = [0, 1777, B - 1]
     sub, seen = _record_eager(lm, [bits[s] for s in sample], ctx, Q_C3)
     for j, s in enumerate(sample):
-        assert sub[j] == toks[s], f"stream {s}: alone (eager) != inside the B={B} graph-replayed batch"
-        assert _oracle_replay(seen, j, bits[s], lm.vocab, Q_C3) == toks[s], f"stream {s}: HIP coder != oracle"
+        assert sub[j] == toks[s], f"{label} stream {s}: alone (eager) != inside the B={B} graph-replayed batch"
+        assert _oracle_replay(seen, j, bits[s], lm.vocab, Q_C3) == toks[s], f"{label} stream {s}: HIP coder != oracle"
+    _free_cache(lm)
+
+
+@pytest.mark.timeout(900)
+def test_c3_gpt2_small_b4096_1kib_roundtrip_bit_exact():
+    _b4096_roundtrip("gpt2", "C3")
+
+
+@pytest.mark.timeout(900)
+def test_c4_gpt2_fa_b4096_share_1kib_roundtrip_bit_exact():
+    """C4 = gpt2-fa, 32,768 streams over 8 GPUs: one GPU's share (4,096 streams) at the gpt2-fa geometry
+    (GPT-2-small layers, V = 42,001, end-of-text 42,000 banned with 628; random-init weights, no checkpoint
+    offline) -- encode -> decode with every payload recovered, and the oracle replay (VERDICT r3 #2)."""
+    _b4096_roundtrip("gpt2-fa", "C4")
 
 
 @pytest.mark.timeout(600)

@@ -243,6 +243,57 @@ def test_non_finite_logits_are_reported(topk, poison):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("dtype,topk,nfinite", [("f32", 300, 150), ("f32", 300, 2), ("f16", 100, 40),
+                                                ("f32", 50000, 3000)])
+def test_masked_rows_match_oracle(dtype, topk, nfinite):
+    """Rows with fewer than topk finite logits (the rest -inf: a caller's mask, or the reference's -1e10 ban
+    overflowing fp16): the -inf ids are ranks of probability 0, so tokens, traces and bits follow the oracle
+    instead of reporting a range error.  NaN rows still do (test above)."""
+    from neuralsteganography_amd.coder import CoderParams, EncodeSession, decode_batch, row_stride
+
+    torch = _torch()
+    V, B, seed = 50257, 3, 29
+    npdt = np.float16 if dtype == "f16" else np.float32
+    precision = 16 if topk > 1000 else 26
+    params = CoderParams(vocab=V, precision=precision, temp=0.9, topk=topk, dtype=dtype)
+    ctx = _ctx(params, B)
+    ld = row_stride(V, dtype)
+
+    def row(s, t):
+        x = synthetic.logits_row(seed, s, t, V, 3.0, npdt).astype(np.float32)
+        keep = np.random.default_rng([seed, s, t]).choice(V, size=nfinite + 7 * s, replace=False)
+        out = np.full(V, -np.inf, np.float32)
+        out[keep] = x[keep]
+        return out
+
+    def fn(t, _last=None):
+        a = np.zeros((B, ld), npdt)
+        for s in range(B):
+            a[s, :V] = row(s, t)
+        return torch.from_numpy(a).cuda()
+
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 6))[: 48 - 5 * s] for s in range(B)]
+    expect = []
+    for s in range(B):
+        toks, tr = oracle.encode_stream(lambda t, s=s: row(s, t), bits[s], banned=params.banned_ids(), temp=0.9,
+                                        precision=precision, topk=topk)
+        expect.append((toks, [(x.k, x.kprime, x.sel, x.n, x.token) for x in tr]))
+    sess = EncodeSession(ctx, bits)
+    sess.enable_trace()
+    for t in range(max(len(e[0]) for e in expect)):
+        sess.step(fn(t))
+        tr = sess.trace_rows()
+        for s in range(B):
+            if t < len(expect[s][1]):
+                got = (int(tr.k[s]), int(tr.kprime[s]), int(tr.sel[s]), int(tr.n[s]), int(tr.token[s]))
+                assert got == expect[s][1][t], f"stream {s} step {t}: kernel {got} oracle {expect[s][1][t]}"
+    toks = sess.tokens()
+    assert toks == [e[0] for e in expect]
+    out = decode_batch(ctx, toks, fn)
+    for s in range(B):
+        assert out[s][: len(bits[s])] == bits[s]
+
+
 def test_empty_and_single_bit_payloads():
     from neuralsteganography_amd.coder import CoderParams, decode_batch, encode_batch, row_stride
 

@@ -105,3 +105,87 @@ def test_stop_candidates_multibyte_last_character_split_across_tokens():
     ascii_tab = stop_candidates(tok, 300, "<eos>")
     assert ascii_tab[ord(">")] and not ascii_tab[0xa9]
     assert int(np.count_nonzero(ascii_tab)) == 1  # only '>' (ids 256..299 decode to bytes 0..43)
+
+
+def test_bpe_repair_merge_past_the_end_restores_the_list():
+    """the reference's longer-token branch (code_base/arithmetic.py:321-333) deletes merged tokens one
+    by one and raises IndexError when the merge reaches the end of the text -- after part of the list was edited.
+    repair_or_restore puts the list back; strict decoding raises DecodeDivergenceError, lenient decoding takes
+    the rank-0 token as unrepairable."""
+    from neuralsteganography_amd.codec.errors import DecodeDivergenceError
+    from neuralsteganography_amd.lm.arithmetic import bpe_repair, repair_or_restore
+
+    class Pieces:
+        pieces = ["a", "b", "c", "abc", "ab"]
+
+        def decode(self, ids):
+            return "".join(self.pieces[int(i)] for i in ids)
+
+        def encode(self, text):
+            out = []
+            while text:  # greedy longest match
+                best = max((i for i, p in enumerate(self.pieces) if text.startswith(p)), key=lambda i: len(self.pieces[i]))
+                out.append(best)
+                text = text[len(self.pieces[best]):]
+            return out
+
+    enc = Pieces()
+    inp = [1, 0, 1, 2]  # "b" "a" "b" "c": candidate "abc" merges the last three tokens
+    with pytest.raises(IndexError):
+        bpe_repair(enc, list(inp), 1, [3, 4])
+    part = list(inp)
+    try:
+        bpe_repair(enc, part, 1, [3, 4])
+    except IndexError:
+        pass
+    assert part != inp  # the reference's loop had edited the list before raising
+    lst = list(inp)
+    assert repair_or_restore(enc, lst, 1, [3, 4], strict=False) == 3 and lst == inp
+    lst = list(inp)
+    with pytest.raises(DecodeDivergenceError):
+        repair_or_restore(enc, lst, 1, [3, 4], strict=True)
+    assert lst == inp
+    lst = list(inp)
+    assert repair_or_restore(enc, lst, 1, [4, 3], strict=True) == 4 and lst == [1, 4, 2]  # "a"+"b" -> "ab"
+
+
+def test_kv_cache_budget_keeps_headroom_and_retries_fragmented_segments(monkeypatch):
+    """VERDICT r3 #9 (CPU-mockable): the cache budget leaves headroom_bytes(B) + the reserve fraction free for
+    what is allocated after the cache, and _allocate_fitted retries with a fresh budget (idle segments released,
+    count_cached=False) when the first request fails on fragmented cached segments (the r03u OOM class)."""
+    from types import SimpleNamespace
+
+    m = random_gpt2("tiny", vocab_size=700, n_positions=64)
+    g = BatchedGPT2(m, device="cpu", compute_dtype=torch.float32)
+    B, GiB = 64, 1 << 30
+    per_pos = g.kv_bytes_per_position(B)
+    g.device = SimpleNamespace(type="cuda")  # the sizing arithmetic only
+    mem = {"free": 40 * GiB, "reserved": 30 * GiB, "allocated": 10 * GiB}
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (mem["free"], 288 * GiB))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda dev=None: mem["reserved"])
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda dev=None: mem["allocated"])
+    want = 10 ** 9
+    got = g.fit_positions(B, want)
+    assert got == (int(60 * GiB * 0.95) - g.headroom_bytes(B)) // per_pos  # idle cached segments count as free
+    assert g.fit_positions(B, want, count_cached=False) == (int(40 * GiB * 0.95) - g.headroom_bytes(B)) // per_pos
+    assert g.fit_positions(B, 5) == 5
+    assert g.headroom_bytes(4096) > g.headroom_bytes(1) > 2 * GiB
+
+    calls, released = [], []
+
+    def fake_allocate(B_, max_len, T0=0, dtype=None, plain=None):
+        calls.append(max_len)
+        if len(calls) == 1:
+            raise torch.OutOfMemoryError("fragmented segments")
+
+    def fake_empty_cache():
+        released.append(True)
+        mem["reserved"] = mem["allocated"]  # idle segments returned to the device
+        mem["free"] += 20 * GiB
+
+    monkeypatch.setattr(g, "allocate", fake_allocate)
+    monkeypatch.setattr(torch.cuda, "empty_cache", fake_empty_cache)
+    g._allocate_fitted(B, 32, want, T0=32)
+    assert released == [True] and len(calls) == 2
+    assert calls[0] == 32 + got
+    assert calls[1] == 32 + (int(60 * GiB * 0.95) - g.headroom_bytes(B)) // per_pos

@@ -183,28 +183,60 @@ def test_crypto_quality_extraction_and_validation():
 
 @pytest.mark.parametrize("name", golden.provider_names())
 def test_oracle_rank_coder_over_generic_providers_matches_reference(name):
-    """encode_with_lm / decode_with_lm over a generic next_token_probs provider (codec/arithmetic.py:122-231):
-    the provider's ProbDist (ndarray or dict) staged as log-probability rows (codec.distribution.probs_to_logits,
-    the rows the GPU path hands the rank kernel) and ranked by the oracle give the reference's tokens and
-    consumption history for the Zipf MockLM and a context-dependent dict provider with a context window."""
-    from neuralsteganography_amd.codec.distribution import dist_to_row, probs_to_logits
-
+    """encode_with_lm / decode_with_lm over a generic next_token_probs provider (codec/arithmetic.py:122-231): the
+    provider's float64 ProbDist (ndarray or dict) ranked, filtered and renormalised by or_rank_step64 (canonical
+    steps P0-P5: the rows the GPU path stages) gives the reference's tokens and consumption history -- the Zipf
+    MockLM, a context-dependent dict provider with a context window, and the near-tie providers whose neighbours
+    differ by 1e-9 .. 1e-8 relative (unnormalised rows, top_p / min_prob boundaries, ids beyond 2^17)."""
     g = golden.load_rank(name)
     m = g.meta
-    win = m.get("max_context")
-    prov = golden.make_provider(m)
-    V = m["vocab"]
     for s in g.streams:
-        def row(t, toks=s.tokens):
-            ctx = list(m["context"]) + list(toks[:t])
-            if win and len(ctx) > win:
-                ctx = ctx[-win:]
-            return probs_to_logits(dist_to_row(prov.next_token_probs(tuple(ctx)), V)[None])[0]
-
-        toks, cons = oracle.rank_encode_stream(row, s.payload, temp=1.0, quality=m["quality"])
+        kw = dict(context=m["context"], quality=m["quality"], max_context=m.get("max_context"))
+        toks, cons = oracle.provider_encode_stream(golden.make_provider(m), s.payload, **kw)
         assert toks == s.tokens and cons == s.consumed, f"{name} stream {s.stream}"
-        dec = oracle.rank_decode_stream(row, toks, cons, 8 * len(s.payload), temp=1.0, quality=m["quality"])
+        dec = oracle.provider_decode_stream(golden.make_provider(m), toks, cons, 8 * len(s.payload), **kw)
         assert dec == s.payload == s.decoded
+
+
+@pytest.mark.parametrize("name", golden.crypto_provider_names())
+def test_oracle_crypto_quality_over_generic_providers_matches_reference(name):
+    """crypto.encode_arithmetic over a generic provider (crypto/arithmetic.py:20-91): the row normalised by
+    numpy's own sum (or_np_sum), tempered / filtered, renormalised (P1-P3), then ranked: the reference's tokens."""
+    g = golden.load_rank(name)
+    m = g.meta
+    for s in g.streams:
+        kw = dict(context=m["context"], quality=m["quality"])
+        toks, cons = oracle.provider_encode_stream(golden.make_provider(m), s.payload, **kw)
+        assert toks == s.tokens and cons == s.consumed, f"{name} stream {s.stream}"
+        dec = oracle.provider_decode_stream(golden.make_provider(m), toks, cons, 8 * len(s.payload), **kw)
+        assert dec == s.payload == s.decoded
+
+
+def test_np_sum_restatement_equals_numpy():
+    """or_np_sum is numpy's float64 sum bit for bit (8192-element chunks of pairwise sums): the normalisation
+    constant the reference divides by (codec/quality.py:174-178, crypto/quality.py)."""
+    import numpy as np
+
+    rng = np.random.default_rng(11)
+    sizes = [0, 1, 7, 8, 9, 127, 128, 129, 1000, 8191, 8192, 8193, 16384, 50257, 131071] + \
+        [int(x) for x in rng.integers(1, 140000, 40)]
+    for n in sizes:
+        a = rng.random(n) ** 7 * 10.0 ** rng.integers(-8, 3, n)
+        assert oracle.np_sum(a) == np.sum(a), n
+        assert oracle.np_sum(a) == a.sum(), n
+
+
+def test_near_tie_rows_merge_at_float32():
+    """The near-tie fixtures separate rows the old float32 log-probability staging merged: adjacent ranked values
+    differ by 1e-9 .. 1e-8 relative, distinct in float64, equal in float32 for most neighbours."""
+    import numpy as np
+
+    from tests.golden.providers import NearTieLM
+
+    p = NearTieLM(scale=0.79).next_token_probs([50256, 1, 2])
+    s = np.sort(p)[::-1]
+    assert np.all(s[:-1] > s[1:])
+    assert (np.float32(np.log(s[:-1])) == np.float32(np.log(s[1:]))).mean() > 0.5
 
 
 def test_kept_mass_is_order_free_and_accurate():
