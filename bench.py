@@ -67,6 +67,8 @@ def parse(argv=None):
                     help="skip the gpt2-fa geometry leg (config C4's per-GPU share: 4096 streams, V = 42,001)")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the C5 per-GPU share: GPT-2-medium fp16, topk 100, temp 0.9, 1024 streams")
+    ap.add_argument("--no-c5-guard", action="store_true",
+                    help="skip the C5 quality-guard-on leg (gated cover generation, pass rate, reveal)")
     ap.add_argument("--no-f16-coder", action="store_true",
                     help="skip the fp16 coder sub-benchmark (the headline's coder kernel: roofline_f16)")
     ap.add_argument("--fp8kv", action="store_true", help="add the fp8-KV-cache end-to-end side line (opt-in mode)")
@@ -315,6 +317,68 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     return out
 
 
+def c5_guard(args, rank, world, dev, n=1024, nbytes=256):
+    """C5's quality guard ON (``cover_generate_batch``, api.py:565-662): GPT-2-medium (random-init, fp16), topk 100,
+    temp 0.9, finish_sent, the reference's regeneration schedule (2 more attempts: next seed, top_k 80 / 70,
+    temp 0.8 / 0.7), n secrets of ``nbytes`` per GPU (one 256-byte packet each).  Random-init weights give no
+    meaningful perplexity, so the gate's max_ppl is the median of an ungated first pass over the same secrets
+    (about half pass at attempt 1; the schedule runs for the rest).  Timed: the gated generation (every attempt's
+    encode + guard scoring); then every passed cover is revealed from its text.  Reports the pass rate per
+    attempt and the reveal's exact fraction."""
+    import torch
+
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.cover import (_ensure_guard, cover_generate_batch, cover_reveal_batch,
+                                               iter_attempts, prepare_gate_thresholds)
+    from neuralsteganography_amd.dist import reduce_job
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from neuralsteganography_amd.stego import normalise_quality
+
+    lm = HipArithmeticLM(random_gpt2("gpt2-medium", seed=77), synthetic.IdTokenizer(50257), device=str(dev),
+                         logits_dtype="f16", max_batch=2 * n)
+    q = {"temp": 0.9, "precision": args.precision, "topk": 100, "finish_sent": True}
+    secrets = [synthetic.payload_bytes(n * rank + s, nbytes) for s in range(n)]
+    seed = "w11. w12. w13"
+    strategy = {"seed_pool": ["w21. w22. w23", "w31. w32. w33"]}
+    first = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=False)
+    guard = _ensure_guard(None)
+    ppl = sorted(v.metrics["ppl"] for v in guard.evaluate_batch(first, prepare_gate_thresholds(None)))
+    gate = {"max_ppl": float(ppl[n // 2])}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=True,
+                               gate_thresholds=gate, regen_attempts=2, regen_strategy=strategy, return_errors=True)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    passed = [i for i, t in enumerate(out) if isinstance(t, str)]
+    attempts = list(iter_attempts(seed, 2, strategy))
+    by_attempt = {}
+    for i in passed:
+        a = next(j for j, att in enumerate(attempts) if out[i].startswith(att.seed_text))
+        by_attempt.setdefault(a, []).append(i)
+    exact = 0
+    t1 = time.perf_counter()
+    for a, idx in sorted(by_attempt.items()):
+        aq = dict(normalise_quality(q), **attempts[a].overrides)
+        got = cover_reveal_batch([out[i] for i in idx], seed_text=attempts[a].seed_text, quality=aq, ecc="rs", lm=lm)
+        exact += sum(1 for i, g in zip(idx, got) if g == secrets[i])
+    torch.cuda.synchronize()
+    rev_s = time.perf_counter() - t1
+    npass_all, n_all, gen_max, _ = reduce_job(len(passed), n, gen_s, 0.0, device=dev)
+    ex_all, _, rev_max, _ = reduce_job(exact, 0, rev_s, 0.0, device=dev)
+    del lm
+    torch.cuda.empty_cache()
+    return {"secrets": int(n_all), "secret_bytes": nbytes, "gate": gate, "seconds": gen_max,
+            "covers_per_s": npass_all / gen_max, "secrets_per_s": n_all / gen_max,
+            "pass_rate": npass_all / max(n_all, 1),
+            "passed_per_attempt": {str(a + 1): len(v) for a, v in sorted(by_attempt.items())},
+            "reveal_exact_fraction": ex_all / max(npass_all, 1), "reveal_seconds": rev_max,
+            "workload": f"gpt2-medium (random-init, fp16) cover_generate_batch, quality guard ON (api default guard, "
+                        f"regeneration schedule api.py:496-523), topk 100, temp 0.9, finish_sent, {n} secrets/GPU x "
+                        f"{nbytes} B; gate max_ppl = median of an ungated pass (random weights)"}
+
+
 def host_logits_rate(args, sess, logits, stream, steps=5):
     """PCIe-inclusive side figure (never `value`): the same coder step when the caller hands over the logit
     batch in pinned host memory, i.e. one H2D copy of [B, ld] per step before ns_encode_step (this GPU only)."""
@@ -530,6 +594,9 @@ def main():
             log("C5 share end to end")
             side["end_to_end_c5"] = end_to_end(args, rank, world, dev, model="gpt2-medium", batch=1024, topk=100,
                                                decode=True)
+        if not args.no_c5_guard:  # C5 with the quality guard ON: gated covers, pass rate, reveal from text
+            log("C5 guard on")
+            side["c5_guard"] = c5_guard(args, rank, world, dev)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             log("fp8 KV end to end")
             side["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")

@@ -22,6 +22,8 @@ struct WideStat {
     uint32_t exact;   // 1: the fast bound is unusable, the CDF kernel computes the exact sum
     uint32_t pad;
     double S_r, B_r, U_r;  // raw streaming sums against r (statistics: row_stats_from_stream)
+    float xt;         // wide_stream_kernel: final collection threshold (segment entries below it are stale)
+    uint32_t nraw;    // wide_stream_kernel: entries written to the stream's segment
 };
 
 }  // namespace nsg

@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
@@ -2351,6 +2352,729 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_TAIL_WAVES_PER_SIMD) void wide_ta
     fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, kin, keys_out, cap, todo, s_keys, s_aux);
 }
 
+// ------------------------------------------------------------------------------------------ wide step, round 4
+// The wide step as two kernels sized for occupancy rather than one workgroup per stream:
+//   wide_stream_kernel  one WAVE per stream (four streams per 256-thread workgroup, like the single-pass coder):
+//                       streams the row once with a 4-tile load ring, keeps the fast sum, the max and the
+//                       running collection threshold x_t = r + T ln(S_part / R) (any partial sum is a lower bound
+//                       of S, so x_t only rises), appends ids at or above it to an 8 KiB LDS buffer, compacts the
+//                       buffer to the current threshold when full and flushes it to the stream's global segment
+//                       (values and ids as two arrays) when it stays more than half full.  At the end: the proven
+//                       fast-sum interval (WideStat) and the final threshold xt; segment entries below xt are stale.
+//   wide_wtail_kernel   one 256-thread workgroup per stream, no key array in LDS: each thread holds up to WT_R
+//                       segment values in registers; pass A: exps, the cutoff (the kept set is x >= vk), the
+//                       order-free limb mass E; pass C: q_i and a 256-bucket histogram (bucket order = rank order)
+//                       of counts and q sums; one prefix per bucket; the members of the searched buckets (overfill,
+//                       selection, the decode token) gathered into LDS and ranked against each other.
+// Anything else -- an ambiguous cutoff or unusable bound (exact sum), k outside [2, topk], a crowded bucket, a
+// decode token that is not kept, an encode range error, more than WT_NL entries -- is handed, untouched, to the
+// device sort + wide_cdf_kernel (the list path) with its collected keys.  Statistics and the sampler keep the
+// one-pass kernel (host dispatch).
+constexpr int WS_WAVES = 4;                    // streams per stream-kernel workgroup
+constexpr int WS_CW = 1024;                    // LDS buffer entries per wave (8 KiB)
+#ifndef NSG_WS_NK
+#define NSG_WS_NK 4  // sample tiles (1,024 fp32 / 2,048 fp16 ids); 8 spill (the unpacked tiles stay live)
+#endif
+constexpr int WT_THREADS = 256;                // tail workgroup
+constexpr int WT_WAVES = WT_THREADS / WAVE;
+constexpr int WT_R = 24;                       // segment entries per tail thread
+constexpr int WT_NL = WT_R * WT_THREADS;       // 6,144
+constexpr int WT_NB = WT_THREADS;              // buckets (one per thread in the prefix)
+constexpr int WT_GM = 256;                     // members of one gathered bucket
+
+__device__ __forceinline__ float* seg_vals(uint64_t* keys, int b, int cap) { return (float*)(keys + (int64_t)b * cap); }
+__device__ __forceinline__ uint32_t* seg_ids(uint64_t* keys, int b, int cap) {
+    return (uint32_t*)(keys + (int64_t)b * cap) + cap;
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+                                                                        unsigned int* count, int cap) {
+    __shared__ uint64_t s_buf[WS_WAVES][WS_CW];
+    constexpr int W = Elem<T>::W;
+    constexpr int TS = WAVE * W;
+    constexpr int WS_NK = NSG_WS_NK;  // sample tiles (in registers during the prologue, skipped by the stream)
+#ifndef NSG_WS_NR
+#define NSG_WS_NR 4
+#endif
+    constexpr int NR = NSG_WS_NR;  // tiles in flight
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WS_WAVES + wv);
+    if (b >= p.B) return;
+    const ns_stream_state st = p.state[b];
+    bool active = !(st.flags & NS_ST_DONE);
+    if (!DECODE && active && st.bit_pos >= p.nbits[b]) {
+        if (lane == 0 && !(p.flags & NS_STEP_FINISH_SENT)) p.state[b].flags = st.flags | NS_ST_DONE;
+        active = false;
+    }
+    if (DECODE && p.active && !p.active[b]) active = false;
+    if (!active) {
+        if (lane == 0) {
+            ws[b].active = 0;
+            count[b] = 0;
+        }
+        return;
+    }
+    NSG_STAMP_RT(p, b, lane, 9);
+    NSG_STAMP(p, b, lane, 0);
+    const int V = p.V;
+    const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+    const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+    const int ntiles = (V + TS - 1) / TS;
+    const double temp = 1.0 / p.inv_temp;
+    const float tempf = (float)temp;
+    const double Rd = (double)(st.hi - st.lo);
+    const float lnthr = (float)(-log(Rd));
+    uint64_t* wbuf = s_buf[wv];
+    float* gv = seg_vals(keys_in, b, cap);
+    uint32_t* gj = seg_ids(keys_in, b, cap);
+
+    // masked ids (past the row, banned): -1e30 and bit q of mb (never collected), bans walked in tile order
+    int bi = 0, next_ban = 0x7FFFFFFF;
+    auto ban_reset = [&]() __attribute__((always_inline)) {
+        bi = 0;
+        next_ban = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
+    };
+    auto load_x = [&](int t, const uint4& raw, float (&x)[W], uint32_t& mb) __attribute__((always_inline)) {
+        Elem<T>::unpack(raw, x);
+        mb = 0u;
+        const int j0 = t * TS + lane * W;
+        if ((t + 1) * TS > V) {
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (j0 + q >= V) {
+                    x[q] = -1.0e30f;
+                    mb |= 1u << q;
+                }
+        }
+        while (next_ban < t * TS) {  // bans of skipped tiles
+            ++bi;
+            next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+        }
+        while (next_ban < (t + 1) * TS) {
+            const int d = next_ban - j0;
+            if (d >= 0 && d < W) {
+#pragma unroll
+                for (int q = 0; q < W; ++q)
+                    if (q == d) {
+                        x[q] = -1.0e30f;
+                        mb |= 1u << q;
+                    }
+            }
+            ++bi;
+            next_ban = bi < p.nbanned ? p.banned[bi] : 0x7FFFFFFF;
+        }
+    };
+    float r = 0.0f, nrc = 0.0f;
+    float m1 = -__builtin_inff();
+    double accS = 0.0, accT = 0.0;
+    float accSf = 0.0f;
+    auto sum_tile = [&](const float (&x)[W]) __attribute__((always_inline)) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 c2 = {p.c32, p.c32}, n2 = {nrc, nrc};
+        f2 a2 = {0.0f, 0.0f}, b2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < W; q += 2) {
+            const f2 x2 = {x[q], x[q + 1]};
+            const f2 t = __builtin_elementwise_fma(x2, c2, n2);
+            const f2 e2 = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            a2 += e2;
+            b2 = __builtin_elementwise_fma(e2, t, b2);
+            m1 = __builtin_fmaxf(__builtin_fmaxf(m1, x[q]), x[q + 1]);
+        }
+        const float a = a2.x + a2.y;
+        accS += (double)a;
+        accT += (double)(b2.x + b2.y);
+        accSf += a;
+    };
+    int cnt = 0;       // entries in the LDS buffer (wave-uniform)
+    uint32_t gcnt = 0;  // entries flushed to the segment
+    float t_wave = -__builtin_inff();
+    auto flush = [&]() __attribute__((always_inline)) {
+        for (int i = lane; i < cnt; i += WAVE) {
+            const uint64_t e = wbuf[i];
+            gv[gcnt + i] = op_raw_val(e);
+            gj[gcnt + i] = (uint32_t)e;
+        }
+        gcnt += (uint32_t)cnt;
+        cnt = 0;
+    };
+    auto append_tile = [&](int t, const float (&x)[W], uint32_t mb) __attribute__((always_inline)) {
+#ifdef NSG_WS_NOAPPEND
+        return;
+#endif
+        uint32_t c = 0u;
+#pragma unroll
+        for (int q = 0; q < W; ++q) c += (x[q] >= t_wave && !((mb >> q) & 1u)) ? 1u : 0u;
+        const uint32_t incl = wave_incl_scan_u32(c);
+        const int tot = __builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        if (tot == 0) return;
+        if (cnt + tot > WS_CW) {
+            cnt = wave_compact(wbuf, cnt, t_wave);
+            if (cnt + tot > WS_CW || 2 * cnt > WS_CW) flush();
+        }
+        uint32_t pos = (uint32_t)cnt + incl - c;
+        const uint32_t j0 = (uint32_t)(t * TS + lane * W);
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            if (x[q] >= t_wave && !((mb >> q) & 1u)) wbuf[pos++] = op_raw(x[q], j0 + q);
+        cnt += tot;
+    };
+    auto threshold = [&](float s_part) __attribute__((always_inline)) -> float {
+        if (!(s_part > 0.0f && s_part < 3.0e38f)) return -__builtin_inff();
+        const float L = __builtin_amdgcn_logf(s_part * 0.9990234375f) * 0.6931471805599453f + lnthr;
+        const float t = r + tempf * L;
+        return t - 1.0e-4f * (1.0f + fabsf(r) + fabsf(tempf * L));
+    };
+
+    // ---- sample: WS_NK whole tiles spread over the row (tile s*space + space-1) give r and the first threshold;
+    // the ring's first tiles are in flight behind them.  Small rows (fewer than 2*WS_NK tiles): r = max of tile 0.
+    const bool spec = ntiles >= 2 * WS_NK;
+    const int space = spec ? ntiles / WS_NK : 1;
+    const int nstream = spec ? ntiles - WS_NK : ntiles;
+    int lt = 0, lc = spec ? space - 1 : 0x7FFFFFFF, sleft = spec ? WS_NK : 0;
+    auto next_tile = [&]() __attribute__((always_inline)) -> int {
+        const int t = lt++;
+        if (--lc == 0) {
+            ++lt;
+            lc = --sleft > 0 ? space - 1 : 0x7FFFFFFF;
+        }
+        return t;
+    };
+    uint4 smp[WS_NK];
+    if (spec) {
+#pragma unroll
+        for (int s = 0; s < WS_NK; ++s) smp[s] = rd.vec((s * space + space - 1) * WAVE + lane);
+    }
+    uint4 ring[NR];
+    int rt[NR];
+#pragma unroll
+    for (int d = 0; d < NR; ++d) {
+        rt[d] = next_tile();
+        ring[d] = rd.vec(rt[d] * WAVE + lane);
+    }
+    float xt_run = -__builtin_inff();
+    if (spec) {
+        float smax = -__builtin_inff();
+        ban_reset();
+#pragma unroll
+        for (int s = 0; s < WS_NK; ++s) {
+            float x[W];
+            uint32_t mb;
+            load_x(s * space + space - 1, smp[s], x, mb);
+#pragma unroll
+            for (int q = 0; q < W; ++q) smax = fmaxf(smax, x[q]);
+        }
+        r = wave_max(smax);
+        if (!(r > -1.0e29f)) r = 0.0f;
+        nrc = -(r * p.c32);
+        ban_reset();
+#pragma unroll
+        for (int s = 0; s < WS_NK; ++s) {
+            float x[W];
+            uint32_t mb;
+            load_x(s * space + space - 1, smp[s], x, mb);
+            sum_tile(x);
+        }
+        xt_run = threshold(wave_sum_f32(accSf));
+        t_wave = xt_run;
+        ban_reset();
+#pragma unroll
+        for (int s = 0; s < WS_NK; ++s) {
+            float x[W];
+            uint32_t mb;
+            load_x(s * space + space - 1, smp[s], x, mb);
+            append_tile(s * space + space - 1, x, mb);
+        }
+    } else {
+        float x[W];
+        uint32_t mb;
+        ban_reset();
+        load_x(0, ring[0], x, mb);
+        float mx = x[0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) mx = fmaxf(mx, x[q]);
+        r = wave_max(mx);
+        if (!(r > -1.0e29f)) r = 0.0f;
+        nrc = -(r * p.c32);
+    }
+    NSG_STAMP(p, b, lane, 1);
+
+    // ---- the stream: ring groups of NR tiles; the threshold rises once per group
+    ban_reset();
+    int pos = 0;
+    for (; pos + NR <= nstream; pos += NR) {
+        // one tile at a time (its slot refilled as soon as it is unpacked): a single tile's values are live
+#pragma unroll
+        for (int d = 0; d < NR; ++d) {
+            const int jt = rt[d];
+            float x[W];
+            uint32_t mb;
+            load_x(jt, ring[d], x, mb);
+            rt[d] = next_tile();
+            ring[d] = rd.vec(rt[d] * WAVE + lane);
+            sum_tile(x);
+            append_tile(jt, x, mb);
+        }
+        xt_run = fmaxf(xt_run, threshold(wave_sum_f32(accSf)));
+        t_wave = xt_run;
+    }
+#pragma unroll
+    for (int d = 0; d < NR; ++d) {
+        if (pos + d < nstream) {
+            float x[W];
+            uint32_t mb;
+            load_x(rt[d], ring[d], x, mb);
+            sum_tile(x);
+            append_tile(rt[d], x, mb);
+        }
+    }
+    NSG_STAMP(p, b, lane, 2);
+
+    // ---- the proven interval, the final threshold, the buffer filtered to it and flushed
+    accS = wave_sum_butterfly(accS);
+    accT = wave_sum_butterfly(accT);
+    float bm1 = wave_max(m1);
+    if (!(bm1 > -1.0e29f)) bm1 = -__builtin_inff();
+    WideStat w;
+    double Sf = 0.0, S_lo = 0.0, S_hi = 0.0;
+    const bool ok = fast_sum_interval_dd(accS, accT, r, (double)(bm1 + 0.0f), p.c32, p.inv_temp, W, Sf, S_lo, S_hi);
+    w.m = bm1;
+    w.m2 = -__builtin_inff();
+    w.r = r;
+    w.active = 1;
+    w.S_lo = S_lo;
+    w.S_hi = S_hi;
+    w.S_fast = Sf;
+    w.exact = (ok && !(p.flags & NS_STEP_FORCE_EXACT_SUM)) ? 0u : 1u;
+    w.pad = 0;
+    w.S_r = accS;
+    w.B_r = 0.0;
+    w.U_r = 0.0;
+    float xt = -__builtin_inff();
+    if (ok) {
+        const double L = log(S_lo / Rd);
+        const double t = (double)w.m + temp * L;
+        xt = (float)(t - 1.0e-4 * (1.0 + fabs((double)w.m) + fabs(temp * L)));
+    }
+    xt = fmaxf(xt, xt_run);
+    t_wave = xt;
+    cnt = wave_compact(wbuf, cnt, t_wave);
+    flush();
+    w.xt = xt;
+    w.nraw = gcnt;
+    if (lane == 0) {
+        ws[b] = w;
+        count[b] = gcnt;
+    }
+    NSG_STAMP(p, b, lane, 3);
+}
+
+// the list path for one stream of the tail kernel: its collected keys (x >= xt) go to keys_out (unsorted) for the
+// device sort; exact: the list kernel computes the exact row sum.  Fewer than two keys (a peaked row whose second
+// largest value is below the running threshold): the row is swept again for x >= min(xt, second largest).
+template <typename T>
+__device__ void wtail_defer(const StepParams& p, WideStat* wsb, int b, const float* gv, const uint32_t* gj, int n,
+                            float xt, uint64_t* keys_out, unsigned int* count, int cap, unsigned int* todo, bool exact,
+                            uint32_t* s_ctr, float* s_top) {
+    const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    uint64_t* ko = keys_out + (int64_t)b * cap;
+    __syncthreads();
+    if (tid == 0) *s_ctr = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += WT_THREADS) {
+        const float v = gv[i];
+        if (v >= xt) ko[atomicAdd(s_ctr, 1u)] = wkey(v, gj[i]);
+    }
+    __syncthreads();
+    uint32_t got = *s_ctr;
+    if (got < 2u && (int)got < p.V - p.nbanned) {
+        // the row's two largest valid values, then every valid id at or above the second one (block sweeps)
+        constexpr int W = Elem<T>::W;
+        const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+        const RowReader rd(rowc, (uint32_t)(p.ld * (int64_t)sizeof(T)));
+        const int nvec = (p.V + W - 1) / W;
+        float l1 = -__builtin_inff(), l2 = -__builtin_inff();
+        for (int v = tid; v < nvec; v += WT_THREADS) {
+            float x[W];
+            Elem<T>::unpack(rd.vec(v), x);
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const int j = v * W + q;
+                const float y = (j < p.V && !is_banned(p, j)) ? x[q] : -__builtin_inff();
+                l2 = fmaxf(l2, fminf(l1, y));
+                l1 = fmaxf(l1, y);
+            }
+        }
+        wave_top2(l1, l2);
+        if (lane == 0) {
+            s_top[2 * wv] = l1;
+            s_top[2 * wv + 1] = l2;
+        }
+        __syncthreads();
+        float b1 = -__builtin_inff(), b2 = -__builtin_inff();
+#pragma unroll
+        for (int i = 0; i < WT_WAVES; ++i) {
+            b2 = fmaxf(fminf(b1, s_top[2 * i]), fmaxf(b2, s_top[2 * i + 1]));
+            b1 = fmaxf(b1, s_top[2 * i]);
+        }
+        const float thr = fminf(xt, b2);
+        if (tid == 0) *s_ctr = 0u;
+        __syncthreads();
+        for (int v = tid; v < nvec; v += WT_THREADS) {
+            float x[W];
+            Elem<T>::unpack(rd.vec(v), x);
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const int j = v * W + q;
+                if (j < p.V && !is_banned(p, j) && x[q] >= thr) {
+                    const uint32_t at = atomicAdd(s_ctr, 1u);
+                    if (at < (uint32_t)cap) ko[at] = wkey(x[q], (uint32_t)j);
+                }
+            }
+        }
+        __syncthreads();
+        got = min(*s_ctr, (uint32_t)cap);
+        if (tid == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 1], 1ull);
+    }
+    if (tid == 0) {
+        count[b] = got;
+        wsb->pad = 1u;
+        if (exact) wsb->exact = 1u;
+        todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
+    }
+}
+
+#ifndef NSG_WT_WAVES_PER_SIMD
+#define NSG_WT_WAVES_PER_SIMD 6
+#endif
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_kernel(
+    StepParams p, WideStat* ws, uint64_t* keys_in, uint64_t* keys_out, unsigned int* count, int cap,
+    unsigned int* todo) {
+    __shared__ uint32_t s_cnt[WT_NB];   // bucket counts, then their exclusive prefix
+    __shared__ uint64_t s_q[WT_NB];     // bucket q sums, then their exclusive prefix
+    __shared__ uint64_t s_mem[WT_GM];   // members of the searched bucket: keys
+    __shared__ int64_t s_memq[WT_GM];   //   and q
+    __shared__ double s_d[4 * WT_WAVES];
+    __shared__ uint64_t s_w[8 * WT_WAVES];
+    __shared__ uint32_t s_ctr[4];
+    __shared__ float s_top[2 * WT_WAVES];
+    __shared__ int64_t s_res[8];
+    const int b = blockIdx.x;
+    WideStat* wsb = &ws[b];
+    const WideStat w = *wsb;
+    if (!w.active) return;
+    const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    NSG_STAMP(p, b, tid, 11);
+    float* gv = seg_vals(keys_in, b, cap);
+    uint32_t* gj = seg_ids(keys_in, b, cap);
+    const float xt = w.xt;
+    int n = (int)w.nraw;
+    const ns_stream_state st = p.state[b];
+    if (w.exact || n > WT_NL) {
+        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, w.exact != 0, s_ctr, s_top);
+        return;
+    }
+    // ---- load: slot r of thread tid = segment entry r * WT_THREADS + tid (stale entries, x < xt, are dropped)
+    float x[WT_R];
+    uint32_t vm = 0u;
+#pragma unroll
+    for (int r = 0; r < WT_R; ++r) {
+        const int i = r * WT_THREADS + tid;
+        x[r] = i < n ? gv[i] : -__builtin_inff();
+        if (i < n && x[r] >= xt) vm |= 1u << r;
+    }
+    s_cnt[tid] = 0u;
+    s_q[tid] = 0ull;
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R, thr = 1.0 / Rd;
+    const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15)), inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
+    const double m = (double)w.m;
+    // ---- A: exps, cutoff, limb mass (the kept set is x >= vk: e is monotone in x)
+    Mass ms{0.0, 0.0, 0.0, 0.0};
+    uint32_t km = 0u, nk = 0u, nv = 0u;
+    bool amb = false;
+    float vk = __builtin_inff();
+#pragma unroll
+    for (int r = 0; r < WT_R; ++r) {
+        if (!((vm >> r) & 1u)) continue;
+        ++nv;
+        const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
+        if (e * inv_lo < thr) continue;
+        amb |= !(e * inv_hi >= thr);
+        km |= 1u << r;
+        ++nk;
+        vk = fminf(vk, x[r]);
+        mass_add(ms, e);
+    }
+    mass_wave_sum(ms);
+    {
+        const uint32_t packed = nk | (nv << 16);  // both <= WT_R * 64 < 2^16
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(packed), WAVE - 1);
+        const float wvk = -wave_max(-vk);
+        const bool wamb = ballot(amb) != 0ull;
+        if (lane == 0) {
+            s_d[4 * wv + 0] = ms.a;
+            s_d[4 * wv + 1] = ms.b;
+            s_d[4 * wv + 2] = ms.c;
+            s_d[4 * wv + 3] = ms.d;
+            s_w[wv] = (uint64_t)tot | ((uint64_t)(wamb ? 1u : 0u) << 32);
+            s_top[wv] = wvk;
+        }
+    }
+    __syncthreads();
+    Mass tot{0.0, 0.0, 0.0, 0.0};
+    int k0 = 0, nvalid = 0;
+    bool amb_a = false;
+    vk = __builtin_inff();
+#pragma unroll
+    for (int i = 0; i < WT_WAVES; ++i) {
+        tot.a += s_d[4 * i + 0];
+        tot.b += s_d[4 * i + 1];
+        tot.c += s_d[4 * i + 2];
+        tot.d += s_d[4 * i + 3];
+        k0 += (int)(s_w[i] & 0xFFFFu);
+        nvalid += (int)((s_w[i] >> 16) & 0xFFFFu);
+        amb_a |= (s_w[i] >> 32) != 0ull;
+        vk = fminf(vk, s_top[i]);
+    }
+    const double E = mass_value(tot);
+    // decode: the received token must be kept (x >= vk), else the list path reports the divergence
+    float xtok = -__builtin_inff();
+    uint64_t kt = 0ull;
+    bool tok_ok = true;
+    if (DECODE) {
+        const int32_t tok = p.in_token[b];
+        tok_ok = tok >= 0 && tok < p.V && !is_banned(p, tok);
+        if (tok_ok) {
+            const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+            xtok = Elem<T>::load1(rowc, tok);
+            kt = wkey(xtok, (uint32_t)tok);
+            tok_ok = xtok >= vk;
+        }
+    }
+    if (amb_a || k0 < 2 || k0 > p.topk || k0 > p.K || !tok_ok || !(E > 0.0 && E <= 1.7976931348623157e308)) {
+        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, amb_a, s_ctr, s_top);
+        return;
+    }
+    NSG_STAMP(p, b, tid, 5);
+    // ---- C: q_i and the bucket histogram over [vk, m] (linear in x: monotone, ties share a bucket)
+    const float fm = w.m;
+    const float bscale = fm > vk ? (float)WT_NB / (fm - vk) : 0.0f;
+    auto bucket_of = [&](float v) __attribute__((always_inline)) -> uint32_t {
+        return min((uint32_t)((fm - v) * bscale), (uint32_t)(WT_NB - 1));
+    };
+#pragma unroll
+    for (int r = 0; r < WT_R; ++r) {
+        if (!((km >> r) & 1u)) continue;
+        const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
+        const uint64_t q = (uint64_t)(int64_t)__builtin_rint((e / E) * Rd);
+        const uint32_t bk = bucket_of(x[r]);
+        atomicAdd(&s_cnt[bk], 1u);
+        atomicAdd((unsigned long long*)&s_q[bk], (unsigned long long)q);
+    }
+    __syncthreads();
+    // ---- prefixes (thread t owns bucket t), the overfill bucket
+    const uint32_t c = s_cnt[tid];
+    const int64_t qv = (int64_t)s_q[tid];
+    const uint32_t ci = wave_incl_scan_u32(c);
+    const int64_t qi = wave_incl_scan(qv, lane);
+    if (lane == WAVE - 1) {
+        s_w[8 + wv] = (uint64_t)qi;
+        s_w[16 + wv] = (uint64_t)ci;
+    }
+    __syncthreads();
+    int64_t qbefore = 0, Q = 0;
+    uint32_t cbefore = 0u;
+#pragma unroll
+    for (int i = 0; i < WT_WAVES; ++i) {
+        const int64_t tq = (int64_t)s_w[8 + i];
+        if (i < wv) {
+            qbefore += tq;
+            cbefore += (uint32_t)s_w[16 + i];
+        }
+        Q += tq;
+    }
+    const int64_t QP = qbefore + qi - qv;
+    const uint32_t CP = cbefore + ci - c;
+    s_cnt[tid] = CP;  // own slot: read above by this thread only
+    s_q[tid] = (uint64_t)QP;
+    int ovf = (Q > (int64_t)R && QP + qv > (int64_t)R) ? tid : WT_NB;
+    ovf = wave_min_int(ovf);
+    if (lane == 0) s_w[24 + wv] = (uint64_t)(uint32_t)ovf;
+    __syncthreads();
+    int b_ov = WT_NB;
+#pragma unroll
+    for (int i = 0; i < WT_WAVES; ++i) b_ov = min(b_ov, (int)(uint32_t)s_w[24 + i]);
+    NSG_STAMP(p, b, tid, 6);
+    // inclusive prefix of bucket bk (the last bucket: Q)
+    auto incl_of = [&](int bk) __attribute__((always_inline)) -> int64_t {
+        return bk + 1 < WT_NB ? (int64_t)s_q[bk + 1] : Q;
+    };
+    // ---- gather the kept members of bucket `bk` (block-uniform) into s_mem / s_memq; returns their count
+    auto gather = [&](int bk) __attribute__((always_inline)) -> int {
+        if (tid == 0) s_ctr[0] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < WT_R; ++r) {
+            if (!((km >> r) & 1u)) continue;
+            if ((int)bucket_of(x[r]) != bk) continue;
+            const uint32_t at = atomicAdd(&s_ctr[0], 1u);
+            if (at < (uint32_t)WT_GM) {
+                const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
+                s_mem[at] = wkey(x[r], gj[r * WT_THREADS + tid]);
+                s_memq[at] = (int64_t)__builtin_rint((e / E) * Rd);
+            }
+        }
+        __syncthreads();
+        return (int)s_ctr[0];
+    };
+    // wave 0: member `lane + 64 j` of the gathered bucket: key, q, rank among the members, cum = inclusive prefix
+    struct Mem {
+        uint64_t key[WT_GM / WAVE];
+        int64_t q[WT_GM / WAVE], cum[WT_GM / WAVE];
+        int rank[WT_GM / WAVE];
+    };
+    auto resolve = [&](int bk, int nm, Mem& mm) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) {
+            const int i = lane + WAVE * j;
+            mm.key[j] = i < nm ? s_mem[i] : 0ull;
+            mm.q[j] = i < nm ? s_memq[i] : 0;
+            mm.rank[j] = 0;
+            mm.cum[j] = 0;
+        }
+        for (int o = 0; o < nm; ++o) {
+            const uint64_t ko = s_mem[o];
+            const int64_t qo = s_memq[o];
+#pragma unroll
+            for (int j = 0; j < WT_GM / WAVE; ++j) {
+                mm.rank[j] += ko > mm.key[j] ? 1 : 0;
+                mm.cum[j] += ko >= mm.key[j] ? qo : 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) mm.cum[j] += (int64_t)s_q[bk];
+    };
+    // ---- overfill: kp = first rank whose cum exceeds R (b_ov == WT_NB: none, kp = k0)
+    int kp = k0, kp_local = WT_GM + 1;
+    int64_t cumkp = Q;
+    if (b_ov < WT_NB) {
+        const int nm = gather(b_ov);
+        if (nm > WT_GM) {  // a crowded bucket (ties, skewed rows): counted like the LDS sort's bitonic fallback
+            if (tid == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 3], 1ull);
+            wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, false, s_ctr, s_top);
+            return;
+        }
+        if (wv == 0) {
+            Mem mm;
+            resolve(b_ov, nm, mm);
+            int kl = WT_GM + 1;
+#pragma unroll
+            for (int j = 0; j < WT_GM / WAVE; ++j)
+                if (lane + WAVE * j < nm && mm.cum[j] > (int64_t)R) kl = min(kl, mm.rank[j]);
+            kl = wave_min_int(kl);
+            int64_t cprev = (int64_t)s_q[b_ov];
+#pragma unroll
+            for (int j = 0; j < WT_GM / WAVE; ++j) {
+                const uint64_t mp = ballot(lane + WAVE * j < nm && mm.rank[j] == kl - 1);
+                if (mp) cprev = (int64_t)readlane_u64((uint64_t)mm.cum[j], __builtin_ctzll(mp));
+            }
+            if (lane == 0) {
+                s_res[0] = kl;
+                s_res[1] = cprev;
+            }
+        }
+        __syncthreads();
+        kp_local = (int)s_res[0];
+        kp = (int)s_cnt[b_ov] + kp_local;
+        cumkp = s_res[1];
+    }
+    const int64_t shift = (int64_t)R - cumkp + (int64_t)st.lo;
+    // ---- the searched bucket: encode, the first bucket (<= b_ov) whose inclusive cum + shift exceeds the payload
+    // index; decode, the token's bucket (it must lie before the overfill point)
+    uint64_t idx = 0ull;
+    int bsel;
+    if (!DECODE) {
+        if (wv == 0) {
+            idx = payload_window(p, b, st.bit_pos);
+            int bl = WT_NB;
+#pragma unroll
+            for (int j = 0; j < WT_NB / WAVE; ++j) {
+                const int bk = lane * (WT_NB / WAVE) + j;
+                if (bk <= b_ov && bk < WT_NB && bl == WT_NB) {
+                    const int64_t inc = bk == b_ov ? cumkp : incl_of(bk);
+                    if ((uint64_t)(inc + shift) > idx) bl = bk;
+                }
+            }
+            bl = wave_min_int(bl);
+            if (lane == 0) {
+                s_res[2] = bl;
+                s_res[3] = (int64_t)idx;
+            }
+        }
+        __syncthreads();
+        bsel = (int)s_res[2];
+        idx = (uint64_t)s_res[3];
+    } else {
+        bsel = (int)bucket_of(xtok);
+    }
+    if (bsel >= WT_NB || bsel > b_ov) {  // encode range error, or a decode token past the overfill point
+        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, false, s_ctr, s_top);
+        return;
+    }
+    int nm = 0;
+    if (bsel != b_ov) {
+        nm = gather(bsel);
+    } else {
+        nm = (int)s_ctr[0];  // still gathered
+    }
+    if (nm > WT_GM) {
+        if (tid == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 3], 1ull);
+        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, false, s_ctr, s_top);
+        return;
+    }
+    int found = 0;
+    if (wv == 0) {
+        Mem mm;
+        resolve(bsel, nm, mm);
+        int rl = WT_GM + 1;
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) {
+            const bool valid = lane + WAVE * j < nm && (bsel != b_ov || mm.rank[j] < kp_local);
+            const bool hit = DECODE ? (valid && mm.key[j] == kt) : (valid && (uint64_t)(mm.cum[j] + shift) > idx);
+            if (hit) rl = min(rl, mm.rank[j]);
+        }
+        rl = wave_min_int(rl);
+        int64_t cum_sel = 0, q_sel = 0;
+        uint64_t key_sel = 0ull;
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) {
+            const uint64_t mh = ballot(lane + WAVE * j < nm && mm.rank[j] == rl);
+            if (mh) {
+                const int src = __builtin_ctzll(mh);
+                cum_sel = (int64_t)readlane_u64((uint64_t)mm.cum[j], src);
+                q_sel = (int64_t)readlane_u64((uint64_t)mm.q[j], src);
+                key_sel = readlane_u64(mm.key[j], src);
+            }
+        }
+        found = rl <= WT_GM;
+        if (found && lane == 0) {
+            const int sel = (int)s_cnt[bsel] + rl;
+            const RowStats rs{0.0, 0.0, 0.0};
+            wide_finish<DECODE>(p, b, st, k0, kp, sel, false, w.S_fast, sel > 0 ? cum_sel - q_sel : 0, cum_sel, shift,
+                                key_sel, m, rs, 0.0, false);
+        }
+        if (lane == 0) s_res[4] = found;
+    }
+    __syncthreads();
+    if (!s_res[4]) wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, false, s_ctr, s_top);
+    NSG_STAMP(p, b, tid, 8);
+    NSG_STAMP_RT(p, b, tid, 10);
+}
+
 // ------------------------------------------------------------------------------------------ rank coder
 // src/neuralstego/codec/arithmetic.py:122-231 (encode_with_lm / decode_with_lm) with apply_quality /
 // cap_bits_per_token (codec/quality.py:57-141).  Two row forms share the quality cut (R2), the capacity cap (R3) and
@@ -2882,11 +3606,35 @@ void nsg_wide_free(ns_ctx* ctx) {
     w = NsgWide();
 }
 
+#ifndef NSG_WIDE_V2
+#define NSG_WIDE_V2 1  // 0: every wide step takes the one-pass kernel
+#endif
 template <typename T, bool DECODE>
 static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
     NsgWide& w = ctx->wide;
     const int B = p.B;
     if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
+    static const int v2 = [] {
+        const char* e = getenv("NSG_WIDE_V2");
+        return e ? atoi(e) : NSG_WIDE_V2;
+    }();
+    if (v2 && !p.sample && !p.stats) {
+        // stream kernel (wave per stream) + tail kernel; only the streams the tail hands on are sorted and listed
+        hipLaunchKernelGGL((nsg::wide_stream_kernel<T, DECODE>), dim3((B + nsg::WS_WAVES - 1) / nsg::WS_WAVES),
+                           dim3(nsg::WS_WAVES * nsg::WAVE), 0, s, p, w.stat, w.keys_in, w.count, w.cap);
+        hipLaunchKernelGGL((nsg::wide_wtail_kernel<T, DECODE>), dim3(B), dim3(nsg::WT_THREADS), 0, s, p, w.stat,
+                           w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+        hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
+                           w.count, w.begin, w.end, 0xFFFFFFFFu, nullptr);
+        size_t bytes = w.sort_tmp_bytes;
+        if (rocprim::segmented_radix_sort_keys_desc(w.sort_tmp, bytes, w.keys_out, w.keys_in,
+                                                    (unsigned int)((size_t)B * w.cap), (unsigned int)B, w.begin,
+                                                    w.end, 0, 49, s) != hipSuccess)
+            return false;
+        hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B < 256 ? B : 256), dim3(nsg::WIDE_THREADS), 0, s,
+                           p, w.stat, w.keys_in, w.count, w.cap, w.todo);
+        return hipGetLastError() == hipSuccess;
+    }
 #if NSG_WIDE_ONEPASS
     hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);

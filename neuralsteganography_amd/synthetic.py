@@ -116,3 +116,25 @@ class SyntheticBatchedLM:
         self.fed.append(tokens.detach().cpu().numpy().copy())
         self.t += 1
         return self._rows()
+
+
+class IdTokenizer:
+    """Synthetic tokenizer for random-init models (no vocabulary file offline): id i <-> " w<i>." (every id but 3
+    ends a sentence), the last id = <|endoftext|>.  ``decode`` / ``encode`` round-trip every id sequence, so covers
+    made with it are revealed from their TEXT (the C5 bench leg and its GPU test)."""
+
+    def __init__(self, vocab: int):
+        self.eos_id = vocab - 1
+
+    def _piece(self, i: int) -> str:
+        return "<|endoftext|>" if i == self.eos_id else f" w{i}" + ("." if i != 3 else "")
+
+    def decode(self, ids, skip_special_tokens: bool = False) -> str:
+        return "".join("" if (skip_special_tokens and int(i) == self.eos_id) else self._piece(int(i)) for i in ids)
+
+    def encode(self, text: str, add_special_tokens: bool = False) -> List[int]:
+        import re
+
+        return [self.eos_id if mm.group(1) is None else int(mm.group(1))
+                for mm in re.finditer(r"<\|endoftext\|>|w(\d+)", text)]
+

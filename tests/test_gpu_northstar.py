@@ -131,24 +131,7 @@ def test_c2_gpt2_small_b1_1kib_oracle_replay_every_step():
         assert out[0][: len(bits[0])] == bits[0]
 
 
-class _IdTokenizer:
-    """id i <-> " w<i>." (every id ends a sentence but 3), last id = <|endoftext|>: decode/encode round-trip
-    every id, so covers are revealed from their text."""
-
-    def __init__(self, vocab):
-        self.eos_id = vocab - 1
-
-    def _piece(self, i):
-        return "<|endoftext|>" if i == self.eos_id else f" w{i}" + ("." if i != 3 else "")
-
-    def decode(self, ids, skip_special_tokens=False):
-        return "".join("" if (skip_special_tokens and int(i) == self.eos_id) else self._piece(int(i)) for i in ids)
-
-    def encode(self, text, add_special_tokens=False):
-        import re
-
-        return [self.eos_id if mm.group(1) is None else int(mm.group(1))
-                for mm in re.finditer(r"<\|endoftext\|>|w(\d+)", text)]
+_IdTokenizer = synthetic.IdTokenizer
 
 
 @pytest.mark.timeout(900)
