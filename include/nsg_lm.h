@@ -57,6 +57,14 @@ int ns_lm_gemm_configs(void);
 int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy, int M,
                     int C, float eps, void* hip_stream);
 
+/* ns_lm_layernorm of d_x (C = K; ln_w, ln_b) followed by ns_lm_gemm of the normalised rows, in ONE launch when
+ * the GEMM is a small-batch one (M <= 16, K <= 1024: every workgroup normalises the M rows into LDS with the
+ * layernorm kernel's arithmetic, bit-identical), else the two kernels with d_a fp16 [M, lda] as the normalised
+ * rows.  Same bits either way (the decode step at B = 1 is bound by launch latency: 24 launches fewer). */
+int ns_lm_ln_gemm(const void* d_x, int64_t ldx, const void* d_ln_w, const void* d_ln_b, float eps, const void* d_wt,
+                  int64_t ldw, const void* d_bias, void* d_y, int64_t ldy, int M, int N, int K, int epilogue,
+                  void* d_a, int64_t lda, void* hip_stream);
+
 /* d_tokens int32 [M]; d_wte fp16 [V, C]; d_wpe fp16 [n_positions, C]; position = L mod n_positions with
  * L = *d_L (int32, device) when d_L is not NULL, else the host value.  Writes d_h fp16 [M, ldh] = wte + wpe
  * and d_a fp16 [M, lda] = layernorm(h; w, b, eps).  Token ids outside [0, V) write NaN rows (the caller

@@ -32,7 +32,7 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
            "ns_decode_attention_fp8", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
-           "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention")
+           "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
 
 
@@ -147,6 +147,8 @@ def lib() -> ctypes.CDLL:
     L.ns_set_split_max_batch.argtypes = [ci]
     L.ns_lm_embed_ln.restype = ci
     L.ns_lm_embed_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_lm_ln_gemm.restype = ci
+    L.ns_lm_ln_gemm.argtypes = [vp, i64, vp, vp, ctypes.c_float, vp, i64, vp, vp, i64, ci, ci, ci, ci, vp, i64, vp]
     L.ns_lm_embed_seq_ln.restype = ci
     L.ns_lm_embed_seq_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
     L.ns_seq_attention.restype = ci

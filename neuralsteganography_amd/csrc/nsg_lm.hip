@@ -937,6 +937,68 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
     ln_row(x, NV4, C, w, b, A + (int64_t)row * lda, eps);
 }
 
+
+// ------------------------------------------------------------------------------------------- LN + direct GEMM
+// LayerNorm fused into the small-batch GEMM (M <= 16, K <= 1024: one chain, the shapes auto_cfg gives the direct
+// kernel): every workgroup normalises the M activation rows itself -- wave w rows w, w + 4, ... with ln_row's
+// arithmetic, so the values are bit-identical to layernorm_kernel's -- into an LDS tile, and its MFMA activation
+// fragments come from there; the weight fragments (the whole K of the wave's 16 rows, <= 32 x 16 B per lane) are
+// issued before the normalisation so their latency hides it.  One launch per LN + GEMM pair instead of two: at
+// B = 1 the decode step is a chain of ~85 launch-latency-bound kernels.
+constexpr int LNG_MAXK = 1024;
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_direct_ln(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ lw,
+                                                      const f16* __restrict__ lb, float eps,
+                                                      const f16* __restrict__ Wt, int64_t ldw,
+                                                      const f16* __restrict__ bias, void* Y, int64_t ldy, int M, int N,
+                                                      int K) {
+    __shared__ __attribute__((aligned(16))) f16 sA[16][LNG_MAXK + 8];  // +16 B per row: conflict-free b128 reads
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = blockIdx.x * 4 + wave;
+    const bool live = nb * 16 < N;
+    const int r = lane & 15, c = lane >> 4;
+    const int KS = K / 32;  // 32-wide k-steps
+    const f16* wrow = Wt + (int64_t)min(nb * 16 + r, N - 1) * ldw + c * 8;
+    f16x8 a[LNG_MAXK / 32];
+    if (live) {
+#pragma unroll
+        for (int u = 0; u < LNG_MAXK / 32; ++u)
+            if (u < KS) a[u] = *(const f16x8*)(wrow + 32 * u);
+    }
+    const int n = nb * 16 + 4 * c;
+    const bool ep = live && n < N;
+    f16x4 pb = {}, ph = {};
+    if (ep) {
+        if (bias) pb = *(const f16x4*)(bias + n);
+        if constexpr (EPI == NS_LM_EPI_RESIDUAL) {
+            if (r < M) ph = *(const f16x4*)((const f16*)Y + (int64_t)r * ldy + n);
+        }
+    }
+    const int NV4 = K >> 2;
+    for (int row = wave; row < M; row += 4) {
+        const f16* xr = X + (int64_t)row * ldx;
+        float x[LN_MAXV][4];
+#pragma unroll
+        for (int v = 0; v < LN_MAXV; ++v) {
+            const int i = lane + 64 * v;
+            if (i < NV4) {
+                const f16x4 t = *(const f16x4*)(xr + 4 * i);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[v][e] = (float)t[e];
+            }
+        }
+        ln_row(x, NV4, K, lw, lb, &sA[row][0], eps);
+    }
+    __syncthreads();
+    if (!ep) return;
+    const f16* arow = &sA[min(r, M - 1)][c * 8];
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < LNG_MAXK / 32; ++u)
+        if (u < KS) acc = mfma16(a[u], *(const f16x8*)(arow + 32 * u), acc);
+    if (r < M) store4_pre<EPI>(Y, ldy, bias != nullptr, pb, ph, r, n, acc);
+}
+
 }  // namespace lm
 }  // namespace nsg
 
@@ -1133,6 +1195,47 @@ extern "C" int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, co
     if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, (const f16*)d_x,
                        ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_ln_gemm(const void* d_x, int64_t ldx, const void* d_lw, const void* d_lb, float eps,
+                             const void* d_wt, int64_t ldw, const void* d_bias, void* d_y, int64_t ldy, int M, int N,
+                             int K, int epilogue, void* d_a, int64_t lda, void* hip_stream) {
+    if (!d_x || !d_lw || !d_lb || !d_wt || !d_y || M <= 0 || N <= 0 || K <= 0) return NS_ERR_CONFIG;
+    const bool fused = M <= 16 && K <= LNG_MAXK && K % 64 == 0 && N % 16 == 0 && auto_cfg(M, N, K) == CFG_DIRECT16;
+    if (!fused) {  // the two kernels, same bits
+        if (!d_a) return NS_ERR_CONFIG;
+        const int rc = ns_lm_layernorm(d_x, ldx, d_lw, d_lb, d_a, lda, M, K, eps, hip_stream);
+        if (rc != NS_OK) return rc;
+        return gemm_checked(d_a, lda, d_wt, ldw, d_bias, d_y, ldy, M, N, K, epilogue, -1, hip_stream);
+    }
+    if (ldx < K || ldw < K || ldy < N) return NS_ERR_CONFIG;
+    const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_wt | (uintptr_t)d_y | (uintptr_t)(d_bias ? d_bias : d_x) |
+                         (uintptr_t)d_lw | (uintptr_t)d_lb;
+    if ((al & 15u) || (ldx & 7) || (ldw & 7) || (ldy & 3)) return NS_ERR_CONFIG;
+    const f16 *x = (const f16*)d_x, *wt = (const f16*)d_wt, *b = (const f16*)d_bias, *lw = (const f16*)d_lw,
+              *lb = (const f16*)d_lb;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    const dim3 grid((N / 16 + 3) / 4);
+    switch (epilogue) {
+        case NS_LM_EPI_STORE:
+            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_STORE>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
+                               d_y, ldy, M, N, K);
+            break;
+        case NS_LM_EPI_GELU:
+            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_GELU>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
+                               d_y, ldy, M, N, K);
+            break;
+        case NS_LM_EPI_RESIDUAL:
+            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_RESIDUAL>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw,
+                               b, d_y, ldy, M, N, K);
+            break;
+        case NS_LM_EPI_STORE_F32:
+            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_STORE_F32>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt,
+                               ldw, b, d_y, ldy, M, N, K);
+            break;
+        default: return NS_ERR_CONFIG;
+    }
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 

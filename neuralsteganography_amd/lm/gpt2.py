@@ -500,11 +500,16 @@ class BatchedGPT2:
         ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
                             self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
                             a.data_ptr(), C, B, C, eps, st), "ns_lm_embed_ln")
+        def ln_gemm(ln_w, ln_b, wt, bias, y, epi, N):  # ln(h) -> GEMM, one launch at small B (same bits)
+            ok(L.ns_lm_ln_gemm(h.data_ptr(), C, ln_w.data_ptr(), ln_b.data_ptr(), eps, wt.data_ptr(), wt.stride(0),
+                               bias.data_ptr(), y.data_ptr(), y.stride(0), B, N, C, epi, a.data_ptr(), C, st),
+               "ns_lm_ln_gemm")
+
         for i, lw in enumerate(self.layers):
             if i > 0:
-                ok(L.ns_lm_layernorm(h.data_ptr(), C, lw["ln1_w"].data_ptr(), lw["ln1_b"].data_ptr(), a.data_ptr(),
-                                     C, B, C, eps, st), "ns_lm_layernorm")
-            gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
+                ln_gemm(lw["ln1_w"], lw["ln1_b"], lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C)
+            else:  # ln_1 of layer 0 comes with the embedding
+                gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
             kc, vc = self.k_cache[i], self.v_cache[i]
             sb, sh, sz = strides[i]
             kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
@@ -515,9 +520,7 @@ class BatchedGPT2:
                             o.stride(0), 1.0 / math.sqrt(D), st)
             ok(rc, "ns_decode_attention_prefix")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
-            ok(L.ns_lm_layernorm(h.data_ptr(), C, lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), a.data_ptr(), C,
-                                 B, C, eps, st), "ns_lm_layernorm")
-            gemm(a, lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C, C)
+            ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)
             gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
         ok(L.ns_lm_layernorm(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B, C,
                              eps, st), "ns_lm_layernorm")

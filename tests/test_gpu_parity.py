@@ -278,7 +278,8 @@ def test_masked_rows_match_oracle(dtype, topk, nfinite):
         toks, tr = oracle.encode_stream(lambda t, s=s: row(s, t), bits[s], banned=params.banned_ids(), temp=0.9,
                                         precision=precision, topk=topk)
         expect.append((toks, [(x.k, x.kprime, x.sel, x.n, x.token) for x in tr]))
-    sess = EncodeSession(ctx, bits)
+    # two finite ids carry at most one bit per token: more tokens than the default history (2 x bits + 64)
+    sess = EncodeSession(ctx, bits, max_tokens=max(len(e[0]) for e in expect) + 8)
     sess.enable_trace()
     for t in range(max(len(e[0]) for e in expect)):
         sess.step(fn(t))

@@ -8,4 +8,5 @@ NSG_WIDE_V2=0 timeout -k 10 120 python -u tools/wide_probe.py > $o/probe_v1.json
 timeout -k 10 500 python -u -m pytest tests/test_gpu_rank_coder.py tests/test_gpu_lm_kernels.py \
   tests/test_gpu_guard.py -m gpu -x -v --timeout 300 --timeout-method thread \
   -k "rank or provider or crypto or queries or generic or seq_attention or native_prefill or invariant or scorer or max_context or cover" \
-  > $o/pytest_new.log 2>&1
+  > $o/pytest_new.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/c2prof -o run --output-format csv -- python tools/c2_probe.py > $o/c2.log 2>&1
