@@ -218,10 +218,11 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
             }
             // one chunk of RPI*NI rows; GENERAL handles the prefix boundary, the clamp past the cache, rows past
             // Lk and the new token from registers -- an interior chunk (all rows stream rows < L0) skips those
-            // selects (same operations on the same values: the bits do not depend on the path)
-            auto chunk = [&](int j0, auto general) {
+            // selects (same operations on the same values: the bits do not depend on the path).  Small batches
+            // (P = 1) issue the next chunk's loads before this chunk's math (register double buffer): a wave's
+            // chunks are otherwise one dependent memory round trip each, which is what a lone stream waits on.
+            auto load_chunk = [&](int j0, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
                 constexpr bool GEN = decltype(general)::value;
-                Raw kr[NI], vr[NI];
 #pragma unroll
                 for (int u = 0; u < NI; ++u) {
                     if constexpr (GEN) {
@@ -238,6 +239,9 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                         vr[u] = __builtin_nontemporal_load((const Raw*)(vb + o));
                     }
                 }
+            };
+            auto math_chunk = [&](int j0, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
+                constexpr bool GEN = decltype(general)::value;
                 float sc[NI];
                 bool valid[NI];
                 float mx = m;
@@ -270,11 +274,46 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                 }
                 m = mx;
             };
-            for (int j0 = s0 + wv * RPI * NI; j0 < Lk; j0 += S * RPI * NI) {
-                if (j0 >= T0 && j0 + RPI * NI <= L0)  // wave-uniform
-                    chunk(j0, std::false_type{});
+            auto interior = [&](int j0) { return j0 >= T0 && j0 + RPI * NI <= L0; };  // wave-uniform
+            const int step = S * RPI * NI;
+            Raw kr[NI], vr[NI];
+            int j0 = s0 + wv * RPI * NI;
+            if constexpr (P > 1) {  // large batches: other waves hide the latency; no second register buffer
+                for (; j0 < Lk; j0 += step) {
+                    if (interior(j0)) {
+                        load_chunk(j0, std::false_type{}, kr, vr);
+                        math_chunk(j0, std::false_type{}, kr, vr);
+                    } else {
+                        load_chunk(j0, std::true_type{}, kr, vr);
+                        math_chunk(j0, std::true_type{}, kr, vr);
+                    }
+                }
+            } else {
+            Raw kn[NI], vn[NI];
+            if (j0 < Lk) {
+                if (interior(j0))
+                    load_chunk(j0, std::false_type{}, kr, vr);
                 else
-                    chunk(j0, std::true_type{});
+                    load_chunk(j0, std::true_type{}, kr, vr);
+            }
+            for (; j0 < Lk; j0 += step) {
+                const int j1 = j0 + step;
+                if (j1 < Lk) {
+                    if (interior(j1))
+                        load_chunk(j1, std::false_type{}, kn, vn);
+                    else
+                        load_chunk(j1, std::true_type{}, kn, vn);
+                }
+                if (interior(j0))
+                    math_chunk(j0, std::false_type{}, kr, vr);
+                else
+                    math_chunk(j0, std::true_type{}, kr, vr);
+#pragma unroll
+                for (int u = 0; u < NI; ++u) {
+                    kr[u] = kn[u];
+                    vr[u] = vn[u];
+                }
+            }
             }
             // merge the row groups (lanes c, c + LPR, ... hold the same dims)
 #pragma unroll

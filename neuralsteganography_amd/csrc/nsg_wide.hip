@@ -2361,13 +2361,13 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_TAIL_WAVES_PER_SIMD) void wide_ta
 //                       buffer to the current threshold when full and flushes it to the stream's global segment
 //                       (values and ids as two arrays) when it stays more than half full.  At the end: the proven
 //                       fast-sum interval (WideStat) and the final threshold xt; segment entries below xt are stale.
-//   wide_wtail_kernel   one 256-thread workgroup per stream, no key array in LDS: each thread holds up to WT_R
-//                       segment values in registers; pass A: exps, the cutoff (the kept set is x >= vk), the
+//   wide_wtail_kernel   one 256-thread workgroup per stream, no key array: each pass streams the segment's values
+//                       again (L2 / Infinity Cache); pass A: exps, the cutoff (the kept set is x >= vk), the
 //                       order-free limb mass E; pass C: q_i and a 256-bucket histogram (bucket order = rank order)
 //                       of counts and q sums; one prefix per bucket; the members of the searched buckets (overfill,
 //                       selection, the decode token) gathered into LDS and ranked against each other.
 // Anything else -- an ambiguous cutoff or unusable bound (exact sum), k outside [2, topk], a crowded bucket, a
-// decode token that is not kept, an encode range error, more than WT_NL entries -- is handed, untouched, to the
+// decode token that is not kept, an encode range error -- is handed, untouched, to the
 // device sort + wide_cdf_kernel (the list path) with its collected keys.  Statistics and the sampler keep the
 // one-pass kernel (host dispatch).
 constexpr int WS_WAVES = 4;                    // streams per stream-kernel workgroup
@@ -2377,8 +2377,7 @@ constexpr int WS_CW = 1024;                    // LDS buffer entries per wave (8
 #endif
 constexpr int WT_THREADS = 256;                // tail workgroup
 constexpr int WT_WAVES = WT_THREADS / WAVE;
-constexpr int WT_R = 24;                       // segment entries per tail thread
-constexpr int WT_NL = WT_R * WT_THREADS;       // 6,144
+constexpr int WT_U = 4;                        // segment values in flight per tail thread
 constexpr int WT_NB = WT_THREADS;              // buckets (one per thread in the prefix)
 constexpr int WT_GM = 256;                     // members of one gathered bucket
 
@@ -2773,19 +2772,25 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     const float xt = w.xt;
     int n = (int)w.nraw;
     const ns_stream_state st = p.state[b];
-    if (w.exact || n > WT_NL) {
-        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, w.exact != 0, s_ctr, s_top);
+    if (w.exact) {
+        wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, true, s_ctr, s_top);
         return;
     }
-    // ---- load: slot r of thread tid = segment entry r * WT_THREADS + tid (stale entries, x < xt, are dropped)
-    float x[WT_R];
-    uint32_t vm = 0u;
+    // every pass streams the segment's values (L2 / Infinity Cache: the stream kernel wrote them just before), WT_U
+    // loads in flight per thread; stale entries (x < xt) are skipped
+    auto for_each = [&](auto&& fn) __attribute__((always_inline)) {
+        for (int i0 = tid; i0 < n; i0 += WT_U * WT_THREADS) {
+            float xv[WT_U];
 #pragma unroll
-    for (int r = 0; r < WT_R; ++r) {
-        const int i = r * WT_THREADS + tid;
-        x[r] = i < n ? gv[i] : -__builtin_inff();
-        if (i < n && x[r] >= xt) vm |= 1u << r;
-    }
+            for (int u = 0; u < WT_U; ++u) {
+                const int i = i0 + u * WT_THREADS;
+                xv[u] = i < n ? gv[i] : -__builtin_inff();
+            }
+#pragma unroll
+            for (int u = 0; u < WT_U; ++u)
+                if (xv[u] >= xt) fn(xv[u], i0 + u * WT_THREADS);
+        }
+    };
     s_cnt[tid] = 0u;
     s_q[tid] = 0ull;
     const uint64_t R = st.hi - st.lo;
@@ -2794,25 +2799,20 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     const double m = (double)w.m;
     // ---- A: exps, cutoff, limb mass (the kept set is x >= vk: e is monotone in x)
     Mass ms{0.0, 0.0, 0.0, 0.0};
-    uint32_t km = 0u, nk = 0u, nv = 0u;
+    uint32_t nk = 0u;
     bool amb = false;
     float vk = __builtin_inff();
-#pragma unroll
-    for (int r = 0; r < WT_R; ++r) {
-        if (!((vm >> r) & 1u)) continue;
-        ++nv;
-        const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
-        if (e * inv_lo < thr) continue;
+    for_each([&](float xv, int) __attribute__((always_inline)) {
+        const double e = exp_canon(((double)xv - m) * p.inv_temp);
+        if (e * inv_lo < thr) return;
         amb |= !(e * inv_hi >= thr);
-        km |= 1u << r;
         ++nk;
-        vk = fminf(vk, x[r]);
+        vk = fminf(vk, xv);
         mass_add(ms, e);
-    }
+    });
     mass_wave_sum(ms);
     {
-        const uint32_t packed = nk | (nv << 16);  // both <= WT_R * 64 < 2^16
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(packed), WAVE - 1);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(nk), WAVE - 1);
         const float wvk = -wave_max(-vk);
         const bool wamb = ballot(amb) != 0ull;
         if (lane == 0) {
@@ -2826,7 +2826,7 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     }
     __syncthreads();
     Mass tot{0.0, 0.0, 0.0, 0.0};
-    int k0 = 0, nvalid = 0;
+    int k0 = 0;
     bool amb_a = false;
     vk = __builtin_inff();
 #pragma unroll
@@ -2835,8 +2835,7 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
         tot.b += s_d[4 * i + 1];
         tot.c += s_d[4 * i + 2];
         tot.d += s_d[4 * i + 3];
-        k0 += (int)(s_w[i] & 0xFFFFu);
-        nvalid += (int)((s_w[i] >> 16) & 0xFFFFu);
+        k0 += (int)(uint32_t)s_w[i];
         amb_a |= (s_w[i] >> 32) != 0ull;
         vk = fminf(vk, s_top[i]);
     }
@@ -2866,15 +2865,14 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     auto bucket_of = [&](float v) __attribute__((always_inline)) -> uint32_t {
         return min((uint32_t)((fm - v) * bscale), (uint32_t)(WT_NB - 1));
     };
-#pragma unroll
-    for (int r = 0; r < WT_R; ++r) {
-        if (!((km >> r) & 1u)) continue;
-        const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
+    for_each([&](float xv, int) __attribute__((always_inline)) {
+        if (!(xv >= vk)) return;  // kept <=> x >= vk
+        const double e = exp_canon(((double)xv - m) * p.inv_temp);
         const uint64_t q = (uint64_t)(int64_t)__builtin_rint((e / E) * Rd);
-        const uint32_t bk = bucket_of(x[r]);
+        const uint32_t bk = bucket_of(xv);
         atomicAdd(&s_cnt[bk], 1u);
         atomicAdd((unsigned long long*)&s_q[bk], (unsigned long long)q);
-    }
+    });
     __syncthreads();
     // ---- prefixes (thread t owns bucket t), the overfill bucket
     const uint32_t c = s_cnt[tid];
@@ -2917,17 +2915,15 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     auto gather = [&](int bk) __attribute__((always_inline)) -> int {
         if (tid == 0) s_ctr[0] = 0u;
         __syncthreads();
-#pragma unroll
-        for (int r = 0; r < WT_R; ++r) {
-            if (!((km >> r) & 1u)) continue;
-            if ((int)bucket_of(x[r]) != bk) continue;
+        for_each([&](float xv, int i) __attribute__((always_inline)) {
+            if (!(xv >= vk) || (int)bucket_of(xv) != bk) return;
             const uint32_t at = atomicAdd(&s_ctr[0], 1u);
             if (at < (uint32_t)WT_GM) {
-                const double e = exp_canon(((double)x[r] - m) * p.inv_temp);
-                s_mem[at] = wkey(x[r], gj[r * WT_THREADS + tid]);
+                const double e = exp_canon(((double)xv - m) * p.inv_temp);
+                s_mem[at] = wkey(xv, gj[i]);
                 s_memq[at] = (int64_t)__builtin_rint((e / E) * Rd);
             }
-        }
+        });
         __syncthreads();
         return (int)s_ctr[0];
     };

@@ -75,7 +75,8 @@ def _b4096_roundtrip(name, label):
     B, nbytes = 4096, 1024
     m = random_gpt2(name, seed=1234)
     lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=B)
-    ctx = synthetic.DEFAULT_CONTEXT
+    # [<|endoftext|>] + 31 ids; the end-of-text id is the vocabulary's last (gpt2-fa: 42,000)
+    ctx = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in range(B)]
     t0 = time.perf_counter()
     toks = lm.encode_batch(bits, ctx, quality=Q_C3)

@@ -1,0 +1,11 @@
+# round 4: wide v2 with the streaming tail: parity, kernel split, timing; C4 / C2 round trips
+set -o pipefail
+o=gpurun_out/r04d; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread \
+  -k "wide or g4 or g5 or 50000 or 60000 or 2000 or masked or non_finite" > $o/pytest_parity.log 2>&1 || exit $?
+NSG_WIDE_V2=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $o/wide -o run --output-format csv -- python tools/wide_probe.py --steps 10 > $o/wide.log 2>&1 || exit $?
+NSG_WIDE_V2=1 timeout -k 10 120 python -u tools/wide_probe.py > $o/probe_v2.jsonl 2>&1 || exit $?
+timeout -k 10 200 python -u -m pytest tests/test_gpu_rank_coder.py -m gpu -x -v --timeout 100 --timeout-method thread \
+  -k "grow" > $o/pytest_grow.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_northstar.py -m gpu -x -v --timeout 500 --timeout-method thread \
+  -k "c4 or c2" > $o/pytest_ns.log 2>&1
