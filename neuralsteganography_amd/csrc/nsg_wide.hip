@@ -2378,18 +2378,28 @@ constexpr int WS_CW = 1024;                    // LDS buffer entries per wave (8
 constexpr int WT_THREADS = 256;                // tail workgroup
 constexpr int WT_WAVES = WT_THREADS / WAVE;
 constexpr int WT_U = 4;                        // segment values in flight per tail thread
+constexpr int WT_LV = 8192;                    // segment values staged in LDS (32 KiB)
 constexpr int WT_NB = WT_THREADS;              // buckets (one per thread in the prefix)
 constexpr int WT_GM = 256;                     // members of one gathered bucket
 
 __device__ __forceinline__ float* seg_vals(uint64_t* keys, int b, int cap) { return (float*)(keys + (int64_t)b * cap); }
+// the id of segment entry i: 16-bit words when the vocabulary fits (V <= 65,536), else 32-bit
+__device__ __forceinline__ uint32_t seg_id(const uint32_t* gj, int i, bool id16) {
+    return id16 ? (uint32_t)((const uint16_t*)gj)[i] : gj[i];
+}
 __device__ __forceinline__ uint32_t* seg_ids(uint64_t* keys, int b, int cap) {
     return (uint32_t*)(keys + (int64_t)b * cap) + cap;
 }
 
 template <typename T, bool DECODE>
 __global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
-                                                                        unsigned int* count, int cap) {
+                                                                        unsigned int* count, int cap,
+                                                                        unsigned int* todo, unsigned int* todo2) {
     __shared__ uint64_t s_buf[WS_WAVES][WS_CW];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's two work lists start empty (no memset launches)
+        todo[0] = 0u;
+        todo2[0] = 0u;
+    }
     constexpr int W = Elem<T>::W;
     constexpr int TS = WAVE * W;
     constexpr int WS_NK = NSG_WS_NK;  // sample tiles (in registers during the prologue, skipped by the stream)
@@ -2428,6 +2438,8 @@ __global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepPara
     uint64_t* wbuf = s_buf[wv];
     float* gv = seg_vals(keys_in, b, cap);
     uint32_t* gj = seg_ids(keys_in, b, cap);
+    uint16_t* gj16 = (uint16_t*)gj;
+    const bool id16 = V <= 65536;  // ids as 16-bit words: 6 bytes per segment entry
 
     // masked ids (past the row, banned): -1e30 and bit q of mb (never collected), bans walked in tile order
     int bi = 0, next_ban = 0x7FFFFFFF;
@@ -2494,7 +2506,10 @@ __global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepPara
         for (int i = lane; i < cnt; i += WAVE) {
             const uint64_t e = wbuf[i];
             gv[gcnt + i] = op_raw_val(e);
-            gj[gcnt + i] = (uint32_t)e;
+            if (id16)
+                gj16[gcnt + i] = (uint16_t)e;
+            else
+                gj[gcnt + i] = (uint32_t)e;
         }
         gcnt += (uint32_t)cnt;
         cnt = 0;
@@ -2684,7 +2699,7 @@ __device__ void wtail_defer(const StepParams& p, WideStat* wsb, int b, const flo
     __syncthreads();
     for (int i = tid; i < n; i += WT_THREADS) {
         const float v = gv[i];
-        if (v >= xt) ko[atomicAdd(s_ctr, 1u)] = wkey(v, gj[i]);
+        if (v >= xt) ko[atomicAdd(s_ctr, 1u)] = wkey(v, seg_id(gj, i, p.V <= 65536));
     }
     __syncthreads();
     uint32_t got = *s_ctr;
@@ -2746,7 +2761,7 @@ __device__ void wtail_defer(const StepParams& p, WideStat* wsb, int b, const flo
 }
 
 #ifndef NSG_WT_WAVES_PER_SIMD
-#define NSG_WT_WAVES_PER_SIMD 6
+#define NSG_WT_WAVES_PER_SIMD 4  // 40 KiB of LDS per workgroup: four per CU
 #endif
 template <typename T, bool DECODE>
 __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_kernel(
@@ -2761,6 +2776,7 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     __shared__ uint32_t s_ctr[4];
     __shared__ float s_top[2 * WT_WAVES];
     __shared__ int64_t s_res[8];
+    __shared__ float s_vals[WT_LV];
     const int b = blockIdx.x;
     WideStat* wsb = &ws[b];
     const WideStat w = *wsb;
@@ -2776,15 +2792,21 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
         wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, true, s_ctr, s_top);
         return;
     }
-    // every pass streams the segment's values (L2 / Infinity Cache: the stream kernel wrote them just before), WT_U
-    // loads in flight per thread; stale entries (x < xt) are skipped
+    // the segment's values are read once into LDS (up to WT_LV of them; a longer segment -- a flat row -- is
+    // streamed from global memory by every pass); stale entries (x < xt) are skipped by every pass
+    const float* src = gv;
+    if (n <= WT_LV) {
+        for (int i = tid; i < n; i += WT_THREADS) s_vals[i] = gv[i];
+        __syncthreads();
+        src = s_vals;
+    }
     auto for_each = [&](auto&& fn) __attribute__((always_inline)) {
         for (int i0 = tid; i0 < n; i0 += WT_U * WT_THREADS) {
             float xv[WT_U];
 #pragma unroll
             for (int u = 0; u < WT_U; ++u) {
                 const int i = i0 + u * WT_THREADS;
-                xv[u] = i < n ? gv[i] : -__builtin_inff();
+                xv[u] = i < n ? src[i] : -__builtin_inff();
             }
 #pragma unroll
             for (int u = 0; u < WT_U; ++u)
@@ -2920,7 +2942,7 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
             const uint32_t at = atomicAdd(&s_ctr[0], 1u);
             if (at < (uint32_t)WT_GM) {
                 const double e = exp_canon(((double)xv - m) * p.inv_temp);
-                s_mem[at] = wkey(xv, gj[i]);
+                s_mem[at] = wkey(xv, seg_id(gj, i, p.V <= 65536));
                 s_memq[at] = (int64_t)__builtin_rint((e / E) * Rd);
             }
         });
@@ -3069,6 +3091,34 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     if (!s_res[4]) wtail_defer<T>(p, wsb, b, gv, gj, n, xt, keys_out, count, cap, todo, false, s_ctr, s_top);
     NSG_STAMP(p, b, tid, 8);
     NSG_STAMP_RT(p, b, tid, 10);
+}
+
+// The streams the tail kernel handed on (todo): up to FAST_NL collected keys are sorted in LDS and finished by
+// fast_tail (the exact row sum in the workgroup when needed); its own hand-offs (errors, non-finite rows) and the
+// longer segments (flat rows: pad stays set, the device-wide sort) go on to wide_cdf_kernel through todo2.  A
+// grid-stride loop over the list, so the launch does not depend on how many there are.
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(FAST_THREADS) void wide_wlist_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+                                                                  uint64_t* keys_out, const unsigned int* count,
+                                                                  int cap, const unsigned int* todo,
+                                                                  unsigned int* todo2) {
+    __shared__ uint64_t s_keys[FAST_NL];
+    __shared__ uint64_t s_aux[FAST_NB / 2];
+    const unsigned int nt = todo[0];
+    for (unsigned int i = blockIdx.x; i < nt; i += gridDim.x) {
+        const int b = (int)todo[1 + i];
+        const int n = (int)count[b];
+        if (n >= 2 && n <= FAST_NL) {
+            const WideStat w = ws[b];
+            __syncthreads();
+            if (threadIdx.x == 0) ws[b].pad = 0u;  // sorted here, not by the device-wide sort
+            fast_tail<T, DECODE, true>(p, w, &ws[b], b, n, KeysFlat{keys_out + (int64_t)b * cap, n}, keys_in, cap,
+                                       todo2, s_keys, s_aux);
+        } else if (threadIdx.x == 0) {
+            todo2[1 + atomicAdd(&todo2[0], 1u)] = (unsigned int)b;
+        }
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------------------------ rank coder
@@ -3572,7 +3622,7 @@ int nsg_wide_alloc(ns_ctx* ctx) {
         hipMalloc((void**)&w.count, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.begin, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.end, ctx->max_batch * sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc((void**)&w.todo, (ctx->max_batch + 1) * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void**)&w.todo, 2 * (ctx->max_batch + 1) * sizeof(unsigned int)) != hipSuccess ||
         hipMalloc((void**)&w.stat, ctx->max_batch * sizeof(nsg::WideStat)) != hipSuccess)
         return NS_ERR_HIP;
     size_t bytes = 0;
@@ -3603,23 +3653,25 @@ void nsg_wide_free(ns_ctx* ctx) {
 }
 
 #ifndef NSG_WIDE_V2
-#define NSG_WIDE_V2 1  // 0: every wide step takes the one-pass kernel
+#define NSG_WIDE_V2 0  // 1: stream + tail kernels (round-4 experiment, measured slower: DESIGN.md §4 wide path)
 #endif
 template <typename T, bool DECODE>
 static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
     NsgWide& w = ctx->wide;
     const int B = p.B;
-    if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
     static const int v2 = [] {
         const char* e = getenv("NSG_WIDE_V2");
         return e ? atoi(e) : NSG_WIDE_V2;
     }();
     if (v2 && !p.sample && !p.stats) {
         // stream kernel (wave per stream) + tail kernel; only the streams the tail hands on are sorted and listed
+        unsigned int* todo2 = w.todo + ctx->max_batch + 1;
         hipLaunchKernelGGL((nsg::wide_stream_kernel<T, DECODE>), dim3((B + nsg::WS_WAVES - 1) / nsg::WS_WAVES),
-                           dim3(nsg::WS_WAVES * nsg::WAVE), 0, s, p, w.stat, w.keys_in, w.count, w.cap);
+                           dim3(nsg::WS_WAVES * nsg::WAVE), 0, s, p, w.stat, w.keys_in, w.count, w.cap, w.todo, todo2);
         hipLaunchKernelGGL((nsg::wide_wtail_kernel<T, DECODE>), dim3(B), dim3(nsg::WT_THREADS), 0, s, p, w.stat,
                            w.keys_in, w.keys_out, w.count, w.cap, w.todo);
+        hipLaunchKernelGGL((nsg::wide_wlist_kernel<T, DECODE>), dim3(B < 512 ? B : 512), dim3(nsg::FAST_THREADS), 0, s,
+                           p, w.stat, w.keys_in, w.keys_out, w.count, w.cap, w.todo, todo2);
         hipLaunchKernelGGL(nsg::wide_offsets_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, w.cap, w.stat,
                            w.count, w.begin, w.end, 0xFFFFFFFFu, nullptr);
         size_t bytes = w.sort_tmp_bytes;
@@ -3628,9 +3680,10 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
                                                     w.end, 0, 49, s) != hipSuccess)
             return false;
         hipLaunchKernelGGL((nsg::wide_cdf_kernel<T, DECODE>), dim3(B < 256 ? B : 256), dim3(nsg::WIDE_THREADS), 0, s,
-                           p, w.stat, w.keys_in, w.count, w.cap, w.todo);
+                           p, w.stat, w.keys_in, w.count, w.cap, todo2);
         return hipGetLastError() == hipSuccess;
     }
+    if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
 #if NSG_WIDE_ONEPASS
     hipLaunchKernelGGL((nsg::wide_onepass_kernel<T, DECODE>), dim3(B), dim3(nsg::FAST_THREADS), 0, s, p, w.stat,
                        w.keys_in, w.keys_out, w.count, w.cap, w.todo);
