@@ -11,10 +11,10 @@ import json
 import statistics
 
 
-def kernel_values(path):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if "coder_step_kernel" in r["Kernel_Name"]]
+def kernel_values(path, kernel="coder_step_kernel"):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
     if not vals:
-        raise SystemExit(f"no coder_step_kernel rows in {path}")
+        raise SystemExit(f"no {kernel} rows in {path}")
     return vals
 
 
@@ -28,11 +28,12 @@ def main():
     ap.add_argument("--vocab", type=int, default=50257)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--topk", type=int, default=300)
+    ap.add_argument("--kernel", default="coder_step_kernel", help="kernel name substring")
     a = ap.parse_args()
-    f = kernel_values(a.fetch_csv)
-    w = kernel_values(a.write_csv)
+    f = kernel_values(a.fetch_csv, a.kernel)
+    w = kernel_values(a.write_csv, a.kernel)
     fetch_kb, write_kb = statistics.mean(f), statistics.mean(w)
-    rec = {"library_version": a.version, "batch": a.batch, "vocab": a.vocab, "dtype": a.dtype, "topk": a.topk,
+    rec = {"library_version": a.version, "kernel": a.kernel, "batch": a.batch, "vocab": a.vocab, "dtype": a.dtype, "topk": a.topk,
            "launches": [len(f), len(w)], "fetch_size_kb_mean": fetch_kb, "write_size_kb_mean": write_kb,
            "read_bytes_corrected": 2.0 * fetch_kb * 1024.0, "write_bytes": write_kb * 1024.0,
            "traffic_bytes_per_launch": 2.0 * fetch_kb * 1024.0 + write_kb * 1024.0,
