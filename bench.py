@@ -317,12 +317,14 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     return out
 
 
-def c5_guard(args, rank, world, dev, n=1024, nbytes=256):
+def c5_guard(args, rank, world, dev, n=1024, max_bytes=256):
     """C5's quality guard ON (``cover_generate_batch``, api.py:565-662): GPT-2-medium (random-init, fp16), topk 100,
     temp 0.9, finish_sent, the reference's regeneration schedule (2 more attempts: next seed, top_k 80 / 70,
-    temp 0.8 / 0.7), n secrets of ``nbytes`` per GPU (one 256-byte packet each).  Random-init weights give no
-    meaningful perplexity, so the gate's max_ppl is the median of an ungated first pass over the same secrets
-    (about half pass at attempt 1; the schedule runs for the rest).  Timed: the gated generation (every attempt's
+    temp 0.8 / 0.7), n secrets of 0 .. max_bytes - 1 bytes per GPU (one packet each; the default guard's unigram
+    metrics reject long covers outright -- a text of a few hundred distinct ids has a unigram entropy above the
+    5.5 limit -- so the secrets span short to long covers).  Random-init weights give no meaningful perplexity,
+    so the gate's max_ppl is the median of an ungated first pass over the same secrets (the schedule runs for the
+    rejected ones).  Timed: the gated generation (every attempt's
     encode + guard scoring); then every passed cover is revealed from its text.  Reports the pass rate per
     attempt and the reveal's exact fraction."""
     import torch
@@ -338,7 +340,7 @@ def c5_guard(args, rank, world, dev, n=1024, nbytes=256):
     lm = HipArithmeticLM(random_gpt2("gpt2-medium", seed=77), synthetic.IdTokenizer(50257), device=str(dev),
                          logits_dtype="f16", max_batch=2 * n)
     q = {"temp": 0.9, "precision": args.precision, "topk": 100, "finish_sent": True}
-    secrets = [synthetic.payload_bytes(n * rank + s, nbytes) for s in range(n)]
+    secrets = [synthetic.payload_bytes(n * rank + s, s % max_bytes) for s in range(n)]
     seed = "w11. w12. w13"
     strategy = {"seed_pool": ["w21. w22. w23", "w31. w32. w33"]}
     first = cover_generate_batch(secrets, seed_text=seed, quality=q, ecc="rs", lm=lm, quality_gate=False)
@@ -369,14 +371,14 @@ def c5_guard(args, rank, world, dev, n=1024, nbytes=256):
     ex_all, _, rev_max, _ = reduce_job(exact, 0, rev_s, 0.0, device=dev)
     del lm
     torch.cuda.empty_cache()
-    return {"secrets": int(n_all), "secret_bytes": nbytes, "gate": gate, "seconds": gen_max,
+    return {"secrets": int(n_all), "secret_bytes": f"0..{max_bytes - 1}", "gate": gate, "seconds": gen_max,
             "covers_per_s": npass_all / gen_max, "secrets_per_s": n_all / gen_max,
             "pass_rate": npass_all / max(n_all, 1),
             "passed_per_attempt": {str(a + 1): len(v) for a, v in sorted(by_attempt.items())},
             "reveal_exact_fraction": ex_all / max(npass_all, 1), "reveal_seconds": rev_max,
             "workload": f"gpt2-medium (random-init, fp16) cover_generate_batch, quality guard ON (api default guard, "
-                        f"regeneration schedule api.py:496-523), topk 100, temp 0.9, finish_sent, {n} secrets/GPU x "
-                        f"{nbytes} B; gate max_ppl = median of an ungated pass (random weights)"}
+                        f"regeneration schedule api.py:496-523), topk 100, temp 0.9, finish_sent, {n} secrets/GPU of "
+                        f"0-{max_bytes - 1} B; gate max_ppl = median of an ungated pass (random weights)"}
 
 
 def host_logits_rate(args, sess, logits, stream, steps=5):

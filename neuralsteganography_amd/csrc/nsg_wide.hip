@@ -2375,6 +2375,10 @@ constexpr int WS_CW = 1024;                    // LDS buffer entries per wave (8
 #ifndef NSG_WS_NK
 #define NSG_WS_NK 4  // sample tiles (1,024 fp32 / 2,048 fp16 ids); 8 spill (the unpacked tiles stay live)
 #endif
+#ifndef NSG_WS_NR
+#define NSG_WS_NR 4
+#endif
+constexpr int WV_CW = 4096;                    // wave-per-stream step: LDS buffer entries (32 KiB)
 constexpr int WT_THREADS = 256;                // tail workgroup
 constexpr int WT_WAVES = WT_THREADS / WAVE;
 constexpr int WT_U = 4;                        // segment values in flight per tail thread
@@ -2391,25 +2395,282 @@ __device__ __forceinline__ uint32_t* seg_ids(uint64_t* keys, int b, int cap) {
     return (uint32_t*)(keys + (int64_t)b * cap) + cap;
 }
 
+// The sort-free tail of one stream by ONE wave, from the candidates in its LDS buffer (wbuf[0, n): raw entries,
+// all at or above the final threshold xt): the arithmetic of wide_wtail_kernel with wave-level reductions.  The
+// step is finished here (state, token / bits) and the stream marked inactive for the later kernels, or handed to
+// the hand-off list (keys to keys_out, pad) for an ambiguous cutoff, k outside [2, topk], a crowded bucket, a decode
+// token that is not kept, or an encode range error.
 template <typename T, bool DECODE>
-__global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
-                                                                        unsigned int* count, int cap,
-                                                                        unsigned int* todo, unsigned int* todo2) {
-    __shared__ uint64_t s_buf[WS_WAVES][WS_CW];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's two work lists start empty (no memset launches)
-        todo[0] = 0u;
-        todo2[0] = 0u;
+__device__ __forceinline__ void wave_tail(const StepParams& p, WideStat* wsb, WideStat w, int b,
+                                          const ns_stream_state& st, const uint64_t* wbuf, int n, uint64_t* keys_out,
+                                          unsigned int* count, int cap, unsigned int* todo) {
+    __shared__ uint32_t t_cnt[WT_NB];  // bucket counts, then their exclusive prefix
+    __shared__ uint64_t t_q[WT_NB];    // bucket q sums, then their exclusive prefix
+    __shared__ uint64_t t_mem[WT_GM];  // gathered members: keys
+    __shared__ int64_t t_memq[WT_GM];  //   and q
+    __shared__ uint32_t t_ctr;
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    auto defer = [&](bool exact) __attribute__((always_inline)) {
+        uint64_t* ko = keys_out + (int64_t)b * cap;
+        for (int i = lane; i < n; i += WAVE) ko[i] = op_raw_key(wbuf[i]);
+        if (lane == 0) {
+            w.pad = 1u;
+            if (exact) w.exact = 1u;
+            w.nraw = 0u;
+            *wsb = w;
+            count[b] = (unsigned int)n;
+            todo[1 + atomicAdd(&todo[0], 1u)] = (unsigned int)b;
+        }
+    };
+    const uint64_t R = st.hi - st.lo;
+    const double Rd = (double)R, thr = 1.0 / Rd;
+    const double inv_lo = 1.0 / (w.S_lo * (1.0 - 1.0e-15)), inv_hi = 1.0 / (w.S_hi * (1.0 + 1.0e-15));
+    const double m = (double)w.m;
+    // ---- A: exps, cutoff (kept <=> x >= vk), order-free limb mass
+    Mass ms{0.0, 0.0, 0.0, 0.0};
+    uint32_t nk = 0u;
+    bool amb = false;
+    float vk = __builtin_inff();
+    for (int i = lane; i < n; i += WAVE) {
+        const float xv = op_raw_val(wbuf[i]);
+        const double e = exp_canon(((double)xv - m) * p.inv_temp);
+        if (e * inv_lo < thr) continue;
+        amb |= !(e * inv_hi >= thr);
+        ++nk;
+        vk = fminf(vk, xv);
+        mass_add(ms, e);
     }
+    mass_wave_sum(ms);
+    const int k0 = __builtin_amdgcn_readlane((int)wave_incl_scan_u32(nk), WAVE - 1);
+    const bool amb_a = ballot(amb) != 0ull;
+    vk = -wave_max(-vk);
+    const double E = mass_value(ms);
+    float xtok = -__builtin_inff();
+    uint64_t kt = 0ull;
+    bool tok_ok = true;
+    if (DECODE) {
+        const int32_t tok = p.in_token[b];
+        tok_ok = tok >= 0 && tok < p.V && !is_banned(p, tok);
+        if (tok_ok) {
+            const char* rowc = (const char*)p.logits + (int64_t)b * p.ld * (int64_t)sizeof(T);
+            xtok = Elem<T>::load1(rowc, tok);
+            kt = wkey(xtok, (uint32_t)tok);
+            tok_ok = xtok >= vk;
+        }
+    }
+    if (amb_a || k0 < 2 || k0 > p.topk || k0 > p.K || !tok_ok || !(E > 0.0 && E <= 1.7976931348623157e308)) {
+        defer(amb_a);
+        return;
+    }
+    // ---- C: q and the bucket histogram over [vk, m]
+    const float fm = w.m;
+    const float bscale = fm > vk ? (float)WT_NB / (fm - vk) : 0.0f;
+    auto bucket_of = [&](float v) __attribute__((always_inline)) -> uint32_t {
+        return min((uint32_t)((fm - v) * bscale), (uint32_t)(WT_NB - 1));
+    };
+    auto q_of = [&](float v) __attribute__((always_inline)) -> int64_t {
+        return (int64_t)__builtin_rint((exp_canon(((double)v - m) * p.inv_temp) / E) * Rd);
+    };
+    for (int j = lane; j < WT_NB; j += WAVE) {
+        t_cnt[j] = 0u;
+        t_q[j] = 0ull;
+    }
+    lds_fence();
+    for (int i = lane; i < n; i += WAVE) {
+        const float xv = op_raw_val(wbuf[i]);
+        if (!(xv >= vk)) continue;
+        const uint32_t bk = bucket_of(xv);
+        atomicAdd(&t_cnt[bk], 1u);
+        atomicAdd((unsigned long long*)&t_q[bk], (unsigned long long)q_of(xv));
+    }
+    lds_fence();
+    // ---- prefixes: lane owns buckets 4 lane .. 4 lane + 3; the overfill bucket
+    constexpr int BPL = WT_NB / WAVE;
+    uint32_t cb[BPL];
+    int64_t qb[BPL];
+    uint32_t csum = 0u;
+    int64_t qsum = 0;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        cb[j] = t_cnt[BPL * lane + j];
+        qb[j] = (int64_t)t_q[BPL * lane + j];
+        csum += cb[j];
+        qsum += qb[j];
+    }
+    const uint32_t cincl = wave_incl_scan_u32(csum);
+    const int64_t qincl = wave_incl_scan(qsum, lane);
+    const int64_t Q = (int64_t)readlane_u64((uint64_t)qincl, WAVE - 1);
+    uint32_t cp = cincl - csum;
+    int64_t qp = qincl - qsum;
+    int ovf = WT_NB;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        t_cnt[BPL * lane + j] = cp;
+        t_q[BPL * lane + j] = (uint64_t)qp;
+        if (Q > (int64_t)R && qp + qb[j] > (int64_t)R && ovf == WT_NB) ovf = BPL * lane + j;
+        cp += cb[j];
+        qp += qb[j];
+    }
+    const int b_ov = wave_min_int(ovf);
+    lds_fence();
+    auto incl_of = [&](int bk) __attribute__((always_inline)) -> int64_t {
+        return bk + 1 < WT_NB ? (int64_t)t_q[bk + 1] : Q;
+    };
+    auto gather = [&](int bk) __attribute__((always_inline)) -> int {
+        if (lane == 0) t_ctr = 0u;
+        lds_fence();
+        for (int i = lane; i < n; i += WAVE) {
+            const uint64_t e = wbuf[i];
+            const float xv = op_raw_val(e);
+            if (!(xv >= vk) || (int)bucket_of(xv) != bk) continue;
+            const uint32_t at = atomicAdd(&t_ctr, 1u);
+            if (at < (uint32_t)WT_GM) {
+                t_mem[at] = op_raw_key(e);
+                t_memq[at] = q_of(xv);
+            }
+        }
+        lds_fence();
+        return (int)__builtin_amdgcn_readfirstlane((int)t_ctr);
+    };
+    struct Mem {
+        uint64_t key[WT_GM / WAVE];
+        int64_t q[WT_GM / WAVE], cum[WT_GM / WAVE];
+        int rank[WT_GM / WAVE];
+    };
+    auto resolve = [&](int bk, int nm, Mem& mm) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) {
+            const int i = lane + WAVE * j;
+            mm.key[j] = i < nm ? t_mem[i] : 0ull;
+            mm.q[j] = i < nm ? t_memq[i] : 0;
+            mm.rank[j] = 0;
+            mm.cum[j] = 0;
+        }
+        for (int o = 0; o < nm; ++o) {
+            const uint64_t ko = t_mem[o];
+            const int64_t qo = t_memq[o];
+#pragma unroll
+            for (int j = 0; j < WT_GM / WAVE; ++j) {
+                mm.rank[j] += ko > mm.key[j] ? 1 : 0;
+                mm.cum[j] += ko >= mm.key[j] ? qo : 0;
+            }
+        }
+        const int64_t base = (int64_t)t_q[bk];
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) mm.cum[j] += base;
+    };
+    auto crowded = [&]() __attribute__((always_inline)) {
+        if (lane == 0 && p.counters) atomicAdd(&p.counters[4 * (b & (NS_COUNTER_SHARDS - 1)) + 3], 1ull);
+        defer(false);
+    };
+    // ---- overfill: kp = first rank whose cum exceeds R
+    int kp = k0, kp_local = WT_GM + 1, nm_ov = -1;
+    int64_t cumkp = Q;
+    if (b_ov < WT_NB) {
+        nm_ov = gather(b_ov);
+        if (nm_ov > WT_GM) {
+            crowded();
+            return;
+        }
+        Mem mm;
+        resolve(b_ov, nm_ov, mm);
+        int kl = WT_GM + 1;
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j)
+            if (lane + WAVE * j < nm_ov && mm.cum[j] > (int64_t)R) kl = min(kl, mm.rank[j]);
+        kl = wave_min_int(kl);
+        int64_t cprev = (int64_t)t_q[b_ov];
+#pragma unroll
+        for (int j = 0; j < WT_GM / WAVE; ++j) {
+            const uint64_t mp = ballot(lane + WAVE * j < nm_ov && mm.rank[j] == kl - 1);
+            if (mp) cprev = (int64_t)readlane_u64((uint64_t)mm.cum[j], __builtin_ctzll(mp));
+        }
+        kp_local = kl;
+        kp = (int)t_cnt[b_ov] + kl;
+        cumkp = cprev;
+    }
+    const int64_t shift = (int64_t)R - cumkp + (int64_t)st.lo;
+    // ---- the searched bucket
+    uint64_t idx = 0ull;
+    int bsel;
+    if (!DECODE) {
+        idx = payload_window(p, b, st.bit_pos);
+        int bl = WT_NB;
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) {
+            const int bk = BPL * lane + j;
+            if (bk <= b_ov && bl == WT_NB) {
+                const int64_t inc = bk == b_ov ? cumkp : incl_of(bk);
+                if ((uint64_t)(inc + shift) > idx) bl = bk;
+            }
+        }
+        bsel = wave_min_int(bl);
+    } else {
+        bsel = (int)bucket_of(xtok);
+    }
+    if (bsel >= WT_NB || bsel > b_ov) {
+        defer(false);
+        return;
+    }
+    const int nm = bsel == b_ov ? nm_ov : gather(bsel);
+    if (nm > WT_GM) {
+        crowded();
+        return;
+    }
+    Mem mm;
+    resolve(bsel, nm, mm);
+    int rl = WT_GM + 1;
+#pragma unroll
+    for (int j = 0; j < WT_GM / WAVE; ++j) {
+        const bool valid = lane + WAVE * j < nm && (bsel != b_ov || mm.rank[j] < kp_local);
+        const bool hit = DECODE ? (valid && mm.key[j] == kt) : (valid && (uint64_t)(mm.cum[j] + shift) > idx);
+        if (hit) rl = min(rl, mm.rank[j]);
+    }
+    rl = wave_min_int(rl);
+    if (rl > WT_GM) {
+        defer(false);
+        return;
+    }
+    int64_t cum_sel = 0, q_sel = 0;
+    uint64_t key_sel = 0ull;
+#pragma unroll
+    for (int j = 0; j < WT_GM / WAVE; ++j) {
+        const uint64_t mh = ballot(lane + WAVE * j < nm && mm.rank[j] == rl);
+        if (mh) {
+            const int src = __builtin_ctzll(mh);
+            cum_sel = (int64_t)readlane_u64((uint64_t)mm.cum[j], src);
+            q_sel = (int64_t)readlane_u64((uint64_t)mm.q[j], src);
+            key_sel = readlane_u64(mm.key[j], src);
+        }
+    }
+    if (lane == 0) {
+        const int sel = (int)t_cnt[bsel] + rl;
+        const RowStats rs{0.0, 0.0, 0.0};
+        wide_finish<DECODE>(p, b, st, k0, kp, sel, false, w.S_fast, sel > 0 ? cum_sel - q_sel : 0, cum_sel, shift,
+                            key_sel, m, rs, 0.0, false);
+        w.active = 0u;  // finished: the tail kernel, the hand-off list and the device sort skip it
+        w.nraw = 0u;
+        *wsb = w;
+        count[b] = 0u;
+    }
+    NSG_STAMP(p, b, lane, 8);
+    NSG_STAMP_RT(p, b, lane, 10);
+}
+
+// NWV waves (streams) per workgroup, CW buffer entries per wave, NR tiles in flight per wave.  INTAIL (the
+// wave-per-stream step, wide_wave_kernel below): a wave whose candidates stayed in its buffer finishes the step
+// itself (wave_tail); the others leave their segment to wide_wtail_kernel.
+template <typename T, bool DECODE, int NWV, int CW, int NR, bool INTAIL>
+__device__ __forceinline__ void wide_stream_body(const StepParams& p, WideStat* ws, uint64_t* keys_in,
+                                                 uint64_t* keys_out, unsigned int* count, int cap,
+                                                 unsigned int* todo, uint64_t (*s_buf)[CW]) {
     constexpr int W = Elem<T>::W;
     constexpr int TS = WAVE * W;
     constexpr int WS_NK = NSG_WS_NK;  // sample tiles (in registers during the prologue, skipped by the stream)
-#ifndef NSG_WS_NR
-#define NSG_WS_NR 4
-#endif
-    constexpr int NR = NSG_WS_NR;  // tiles in flight
+    constexpr int WS_CW = CW;
     const int lane = (int)(threadIdx.x & (WAVE - 1));
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WS_WAVES + wv);
+    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * NWV + wv);
     if (b >= p.B) return;
     const ns_stream_state st = p.state[b];
     bool active = !(st.flags & NS_ST_DONE);
@@ -2675,14 +2936,50 @@ __global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepPara
     xt = fmaxf(xt, xt_run);
     t_wave = xt;
     cnt = wave_compact(wbuf, cnt, t_wave);
-    flush();
     w.xt = xt;
+    if constexpr (INTAIL) {
+        // every candidate is still in the buffer: this wave finishes the step (else the segment goes to the tail
+        // kernel, which also takes the exact row sum and the sweep for a peaked row)
+        if (gcnt == 0 && !w.exact && cnt >= 2) {
+            NSG_STAMP(p, b, lane, 3);
+            wave_tail<T, DECODE>(p, &ws[b], w, b, st, wbuf, cnt, keys_out, count, cap, todo);
+            return;
+        }
+    }
+    flush();
     w.nraw = gcnt;
     if (lane == 0) {
         ws[b] = w;
         count[b] = gcnt;
     }
     NSG_STAMP(p, b, lane, 3);
+}
+
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WS_WAVES* WAVE, 4) void wide_stream_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+                                                                        unsigned int* count, int cap,
+                                                                        unsigned int* todo, unsigned int* todo2) {
+    __shared__ uint64_t s_buf[WS_WAVES][WS_CW];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's two work lists start empty (no memset launches)
+        todo[0] = 0u;
+        todo2[0] = 0u;
+    }
+    wide_stream_body<T, DECODE, WS_WAVES, WS_CW, NSG_WS_NR, false>(p, ws, keys_in, nullptr, count, cap, todo, s_buf);
+}
+
+// the wave-per-stream step: one 64-thread workgroup per stream, a WV_CW-entry LDS buffer (its ~4,000 kept ids
+// stay on chip), a WV_NR-tile load ring (one wave per SIMD: the ring is what keeps bytes in flight), the tail in
+// the same wave
+#ifndef NSG_WV_NR
+#define NSG_WV_NR 12
+#endif
+template <typename T, bool DECODE>
+__global__ __launch_bounds__(WAVE, 1) void wide_wave_kernel(StepParams p, WideStat* ws, uint64_t* keys_in,
+                                                            uint64_t* keys_out, unsigned int* count, int cap,
+                                                            unsigned int* todo, unsigned int* todo2) {
+    __shared__ uint64_t s_buf[1][WV_CW];
+    if (blockIdx.x == 0 && threadIdx.x == 0) todo2[0] = 0u;  // the hand-off kernel's list (todo: memset before)
+    wide_stream_body<T, DECODE, 1, WV_CW, NSG_WV_NR, true>(p, ws, keys_in, keys_out, count, cap, todo, s_buf);
 }
 
 // the list path for one stream of the tail kernel: its collected keys (x >= xt) go to keys_out (unsorted) for the
@@ -2780,7 +3077,7 @@ __global__ __launch_bounds__(WT_THREADS, NSG_WT_WAVES_PER_SIMD) void wide_wtail_
     const int b = blockIdx.x;
     WideStat* wsb = &ws[b];
     const WideStat w = *wsb;
-    if (!w.active) return;
+    if (!w.active || w.pad) return;  // finished by the wave-per-stream step, or already on the hand-off list
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     NSG_STAMP(p, b, tid, 11);
     float* gv = seg_vals(keys_in, b, cap);
@@ -3664,10 +3961,19 @@ static bool wide_launch_t(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) 
         return e ? atoi(e) : NSG_WIDE_V2;
     }();
     if (v2 && !p.sample && !p.stats) {
-        // stream kernel (wave per stream) + tail kernel; only the streams the tail hands on are sorted and listed
+        // v2 = 1: stream kernel (wave per stream, 8 KiB buffers) + tail kernel; v2 = 2: wave per stream with the
+        // tail in the same wave (32 KiB buffers), the tail kernel only for the streams whose buffer overflowed.
+        // Only the streams the tails hand on are sorted and listed.
         unsigned int* todo2 = w.todo + ctx->max_batch + 1;
-        hipLaunchKernelGGL((nsg::wide_stream_kernel<T, DECODE>), dim3((B + nsg::WS_WAVES - 1) / nsg::WS_WAVES),
-                           dim3(nsg::WS_WAVES * nsg::WAVE), 0, s, p, w.stat, w.keys_in, w.count, w.cap, w.todo, todo2);
+        if (v2 == 2) {
+            if (hipMemsetAsync(w.todo, 0, sizeof(unsigned int), s) != hipSuccess) return false;
+            hipLaunchKernelGGL((nsg::wide_wave_kernel<T, DECODE>), dim3(B), dim3(nsg::WAVE), 0, s, p, w.stat,
+                               w.keys_in, w.keys_out, w.count, w.cap, w.todo, todo2);
+        } else {
+            hipLaunchKernelGGL((nsg::wide_stream_kernel<T, DECODE>), dim3((B + nsg::WS_WAVES - 1) / nsg::WS_WAVES),
+                               dim3(nsg::WS_WAVES * nsg::WAVE), 0, s, p, w.stat, w.keys_in, w.count, w.cap, w.todo,
+                               todo2);
+        }
         hipLaunchKernelGGL((nsg::wide_wtail_kernel<T, DECODE>), dim3(B), dim3(nsg::WT_THREADS), 0, s, p, w.stat,
                            w.keys_in, w.keys_out, w.count, w.cap, w.todo);
         hipLaunchKernelGGL((nsg::wide_wlist_kernel<T, DECODE>), dim3(B < 512 ? B : 512), dim3(nsg::FAST_THREADS), 0, s,
