@@ -45,6 +45,9 @@
 #ifndef NSG_ASM_APPEND
 #define NSG_ASM_APPEND 0
 #endif
+#ifndef NSG_SETBIT_APPEND
+#define NSG_SETBIT_APPEND 0  // 1: per-lane pass masks and a set-bit loop per tile (A/B)
+#endif
 #ifndef NSG_DIAG_NOWRITE
 #define NSG_DIAG_NOWRITE 0
 #endif
@@ -310,10 +313,21 @@ template <int W, int G>
 __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], const int (&tb)[G], int lj, int K,
                                             int lane) {
     int n = 0;
+#if NSG_SETBIT_APPEND
+    uint32_t pm[G];  // per tile: bit q = value q passes
+#pragma unroll
+    for (int d = 0; d < G; ++d) {
+        pm[d] = 0u;
+#pragma unroll
+        for (int q = 0; q < W; ++q) pm[d] |= (x[d][q] > c.thr) ? (1u << q) : 0u;
+        n += __builtin_popcount(pm[d]);
+    }
+#else
 #pragma unroll
     for (int d = 0; d < G; ++d)
 #pragma unroll
         for (int q = 0; q < W; ++q) n += (x[d][q] > c.thr) ? 1 : 0;
+#endif
     int excl, total;
     wave_excl_prefix(n, excl, total);
     if (total == 0) return;
@@ -349,6 +363,29 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
                 : "memory");
             pos += pass ? 1 : 0;
         }
+#elif NSG_SETBIT_APPEND
+    // per tile, a wave-uniform loop over the lanes' set pass bits (as many rounds as the most passes any lane has
+    // in the tile: usually one) instead of one predicated write per value slot; the value comes from the tile's W
+    // registers through a select tree on the bit index
+#pragma unroll
+    for (int d = 0; d < G; ++d) {
+        uint32_t m = pm[d];
+        while (ballot(m != 0u)) {
+            if (m) {
+                const uint32_t q = (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                float sv[W];
+#pragma unroll
+                for (int i = 0; i < W; ++i) sv[i] = x[d][i];
+#pragma unroll
+                for (int k = 0; (1 << k) < W; ++k)
+#pragma unroll
+                    for (int i = 0; i < (W >> (k + 1)); ++i) sv[i] = ((q >> k) & 1u) ? sv[2 * i + 1] : sv[2 * i];
+                c.keys[pos] = raw_entry(sv[0], (uint32_t)(tb[d] + lj) + q);
+                ++pos;
+            }
+        }
+    }
 #else
 #pragma unroll
     for (int d = 0; d < G; ++d)

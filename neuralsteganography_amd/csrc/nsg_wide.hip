@@ -1601,7 +1601,7 @@ __device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* ws
     auto e_of = [&](uint64_t k) __attribute__((always_inline)) -> double {
         return exp_canon(((double)wkey_val(k) - m) * p.inv_temp);
     };
-    uint32_t vm = 0u, km = 0u;
+    uint32_t km = 0u;
     Mass ms{0.0, 0.0, 0.0, 0.0};
     uint64_t kmin = ~0ull, kmax = 0ull;
     uint32_t nk = 0u;
@@ -1610,7 +1610,6 @@ __device__ __noinline__ bool nosort_tail(const StepParams& p, const WideStat* ws
     for (int r = 0; r < FAST_R; ++r) {
         uint64_t k;
         if (!kin(r, k)) continue;
-        vm |= 1u << r;
         kmax = k > kmax ? k : kmax;
         const double e = e_of(k);
         if (e * inv_lo < thr) continue;  // provably below the cutoff
@@ -2250,7 +2249,8 @@ __global__ __launch_bounds__(FAST_THREADS, NSG_FAST_WAVES_PER_SIMD) void wide_on
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
     };
 
-    int n = 0, n_before = 0;
+    int n = 0;
+    [[maybe_unused]] int n_before = 0;  // wave w's offset in the segment (split form only)
     bool from_lds = false;
     if (!any_ovf) {
         // ---- each wave filters its buffer to x >= xt_all in place; fast_tail reads the kept keys of its own
