@@ -31,7 +31,7 @@ namespace nsg {
 #endif
 
 constexpr int ATT_D = 64;
-constexpr int ATT_U = 4;      // 8-row chunks per loop iteration: 32 keys per wave in flight
+
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
