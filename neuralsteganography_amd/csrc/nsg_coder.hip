@@ -45,6 +45,9 @@
 #ifndef NSG_ASM_APPEND
 #define NSG_ASM_APPEND 0
 #endif
+#ifndef NSG_F16_NATIVE
+#define NSG_F16_NATIVE 0  // 1: fp16 groups kept packed (fma_mix exponents, fp16 compares, set-bit appends; A/B)
+#endif
 #ifndef NSG_SETBIT_APPEND
 #define NSG_SETBIT_APPEND 0  // 1: per-lane pass masks and a set-bit loop per tile (A/B)
 #endif
@@ -396,6 +399,72 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
                 ++pos;
             }
 #endif
+    c.cnt += total;
+}
+
+// ---- fp16 rows kept packed (NSG_F16_NATIVE): the fast-sum exponent from the halves (the conversion folds into
+// v_fma_mix), the candidate test as an fp16 compare against the largest half <= thr (x > thr <=> x > that half
+// for every half x), and the passing values picked by a set-bit loop and converted one by one -- instead of
+// converting all 32 values of a group to fp32 first.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2v as_h2(uint32_t w) { return __builtin_bit_cast(h2v, w); }
+__device__ __forceinline__ _Float16 half_below(float t) {  // the largest half <= t (t not NaN)
+    _Float16 h = (_Float16)t;
+    if ((float)h > t) {
+        uint16_t u = __builtin_bit_cast(uint16_t, h);
+        if (u == 0x0000u) u = 0x8001u;         // +0 -> -smallest denormal
+        else if (u & 0x8000u) u = (uint16_t)(u + 1u);  // negative: one ulp further from zero
+        else u = (uint16_t)(u - 1u);           // positive (incl. +inf -> max finite): one ulp toward zero
+        h = __builtin_bit_cast(_Float16, u);
+    }
+    return h;
+}
+template <int G>
+__device__ __forceinline__ void offer_group_h(Cand& c, const uint4 (&raw)[G], const int (&tb)[G], int lj, int K,
+                                              int lane) {
+    const _Float16 t16 = half_below(c.thr);
+    uint32_t pm[G];
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < G; ++d) {
+        const uint32_t wd[4] = {raw[d].x, raw[d].y, raw[d].z, raw[d].w};
+        uint32_t m = 0u;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const h2v h = as_h2(wd[w]);
+            m |= (h.x > t16 ? 1u : 0u) << (2 * w);
+            m |= (h.y > t16 ? 1u : 0u) << (2 * w + 1);
+        }
+        pm[d] = m;
+        n += __builtin_popcount(m);
+    }
+    int excl, total;
+    wave_excl_prefix(n, excl, total);
+    if (total == 0) return;
+    if (c.cnt + total > CAND) {  // the per-tile path (compacts as needed) on fp32 values
+#pragma unroll
+        for (int d = 0; d < G; ++d) {
+            float x[8];
+            Elem<_Float16>::unpack(raw[d], x);
+            offer<8>(c, x, tb[d] + lj, K, lane);
+        }
+        return;
+    }
+    int pos = c.cnt + excl;
+#pragma unroll
+    for (int d = 0; d < G; ++d) {
+        uint32_t m = pm[d];
+        while (ballot(m != 0u)) {
+            if (m) {
+                const uint32_t q = (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                const uint32_t wsel = (q & 4u) ? ((q & 2u) ? raw[d].w : raw[d].z) : ((q & 2u) ? raw[d].y : raw[d].x);
+                const float v = Elem<_Float16>::h2f((q & 1u) ? (wsel >> 16) : (wsel & 0xFFFFu));
+                c.keys[pos] = raw_entry(v, (uint32_t)(tb[d] + lj) + q);
+                ++pos;
+            }
+        }
+    }
     c.cnt += total;
 }
 
@@ -887,6 +956,44 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     // range-checked by the buffer descriptor and return zeros.
     int pos = 0;
     for (; pos + PREFETCH <= nstream; pos += PREFETCH) {
+        if constexpr (NSG_F16_NATIVE && sizeof(T) == 2 && !STATS) {
+            uint4 raw[PREFETCH];
+            int jt[PREFETCH], tb[PREFETCH];
+#pragma unroll
+            for (int d = 0; d < PREFETCH; ++d) {
+                raw[d] = buf[d];
+                jt[d] = tid[d];
+                tb[d] = jt[d] * TS;
+                tid[d] = next_tile();
+                buf[d] = rd.vec(tid[d] * WAVE + lane);
+            }
+            if (!(jt[PREFETCH - 1] == ntiles - 1 || next_ban < (jt[PREFETCH - 1] + 1) * TS)) {
+                // the usual group: no masked id, values stay packed
+                float a = 0.0f, a1 = 0.0f;
+#pragma unroll
+                for (int d = 0; d < PREFETCH; ++d) {
+                    const uint32_t wd[4] = {raw[d].x, raw[d].y, raw[d].z, raw[d].w};
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const h2v h = as_h2(wd[w]);
+                        a += __builtin_amdgcn_exp2f(__builtin_fmaf((float)h.x, c32, nrc));
+                        a1 += __builtin_amdgcn_exp2f(__builtin_fmaf((float)h.y, c32, nrc));
+                    }
+                }
+                acc64 += (double)(a + a1);
+                offer_group_h<PREFETCH>(cand, raw, tb, lane * W, K, lane);
+                continue;
+            }
+            float xg[PREFETCH][W];
+#pragma unroll
+            for (int d = 0; d < PREFETCH; ++d) {
+                Elem<T>::unpack(raw[d], xg[d]);
+                mask_tile<W>(p, xg[d], jt[d], ntiles, tb[d] + lane * W, bi, next_ban);
+            }
+            accumulate(&xg[0][0], PREFETCH * W);
+            offer_group<W, PREFETCH>(cand, xg, tb, lane * W, K, lane);
+            continue;
+        }
         float xg[PREFETCH][W];
         int jt[PREFETCH], tb[PREFETCH];
 #pragma unroll
