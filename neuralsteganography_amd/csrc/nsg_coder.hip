@@ -49,7 +49,7 @@
 #define NSG_F16_NATIVE 0  // 1: fp16 groups kept packed (fma_mix exponents, fp16 compares, set-bit appends; A/B)
 #endif
 #ifndef NSG_SETBIT_APPEND
-#define NSG_SETBIT_APPEND 0  // 1: per-lane pass masks and a set-bit loop per tile (A/B)
+#define NSG_SETBIT_APPEND 2  // per-lane pass masks + a set-bit loop per tile: 0 never, 1 always, 2 fp16 rows only
 #endif
 #ifndef NSG_DIAG_NOWRITE
 #define NSG_DIAG_NOWRITE 0
@@ -315,22 +315,24 @@ __device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
 template <int W, int G>
 __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], const int (&tb)[G], int lj, int K,
                                             int lane) {
+    // set-bit appends: measured 1.6-2.2 % faster on fp16 rows, 2 % slower on fp32 rows (profiles/r04/coder_append_ab.jsonl)
+    constexpr bool SETBIT = NSG_SETBIT_APPEND == 1 || (NSG_SETBIT_APPEND == 2 && W == 8);
     int n = 0;
-#if NSG_SETBIT_APPEND
-    uint32_t pm[G];  // per tile: bit q = value q passes
+    uint32_t pm[G];  // SETBIT, per tile: bit q = value q passes
+    if constexpr (SETBIT) {
 #pragma unroll
-    for (int d = 0; d < G; ++d) {
-        pm[d] = 0u;
+        for (int d = 0; d < G; ++d) {
+            pm[d] = 0u;
 #pragma unroll
-        for (int q = 0; q < W; ++q) pm[d] |= (x[d][q] > c.thr) ? (1u << q) : 0u;
-        n += __builtin_popcount(pm[d]);
+            for (int q = 0; q < W; ++q) pm[d] |= (x[d][q] > c.thr) ? (1u << q) : 0u;
+            n += __builtin_popcount(pm[d]);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < G; ++d)
+#pragma unroll
+            for (int q = 0; q < W; ++q) n += (x[d][q] > c.thr) ? 1 : 0;
     }
-#else
-#pragma unroll
-    for (int d = 0; d < G; ++d)
-#pragma unroll
-        for (int q = 0; q < W; ++q) n += (x[d][q] > c.thr) ? 1 : 0;
-#endif
     int excl, total;
     wave_excl_prefix(n, excl, total);
     if (total == 0) return;
@@ -366,7 +368,8 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
                 : "memory");
             pos += pass ? 1 : 0;
         }
-#elif NSG_SETBIT_APPEND
+#else
+    if constexpr (SETBIT) {
     // per tile, a wave-uniform loop over the lanes' set pass bits (as many rounds as the most passes any lane has
     // in the tile: usually one) instead of one predicated write per value slot; the value comes from the tile's W
     // registers through a select tree on the bit index
@@ -389,7 +392,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
             }
         }
     }
-#else
+    } else {
 #pragma unroll
     for (int d = 0; d < G; ++d)
 #pragma unroll
@@ -398,6 +401,7 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
                 c.keys[pos] = raw_entry(x[d][q], (uint32_t)(tb[d] + lj + q));
                 ++pos;
             }
+    }
 #endif
     c.cnt += total;
 }
