@@ -32,7 +32,9 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
            "ns_decode_attention_fp8", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
-           "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm")
+           "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm",
+           "ns_frac_create", "ns_frac_destroy", "ns_frac_last_error", "ns_frac_init", "ns_frac_encode_step",
+           "ns_frac_decode_step")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
 
 
@@ -153,6 +155,18 @@ def lib() -> ctypes.CDLL:
     L.ns_lm_embed_seq_ln.argtypes = [vp, vp, vp, ci, ci, ci, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
     L.ns_seq_attention.restype = ci
     L.ns_seq_attention.argtypes = [vp, i64, vp, i64, ci, ci, ci, ci, ctypes.c_float, vp]
+    L.ns_frac_create.restype = vp
+    L.ns_frac_create.argtypes = [ci, ci, ci]
+    L.ns_frac_destroy.restype = None
+    L.ns_frac_destroy.argtypes = [vp]
+    L.ns_frac_last_error.restype = ctypes.c_char_p
+    L.ns_frac_last_error.argtypes = [vp]
+    L.ns_frac_init.restype = ci
+    L.ns_frac_init.argtypes = [vp, ci, vp, vp]
+    L.ns_frac_encode_step.restype = ci
+    L.ns_frac_encode_step.argtypes = [vp, ci, vp, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, vp]
+    L.ns_frac_decode_step.restype = ci
+    L.ns_frac_decode_step.argtypes = [vp, ci, vp, vp, i64, vp, vp, vp, i64, i64, vp, i64, vp, vp, vp]
     _lib = L
     return L
 
