@@ -52,7 +52,10 @@ def _dist_row(dist) -> Tuple[np.ndarray, np.ndarray]:
     order, or the dict's sorted items), raising what its ``_to_fraction`` (``:545-550``) raises for the first
     value it cannot take: a negative value, then NaN / infinity (``Fraction.from_float``)."""
     if isinstance(dist, np.ndarray):
-        vals = np.asarray([float(v) for v in dist.tolist()], dtype=np.float64)
+        if dist.ndim == 1 and dist.dtype.kind in "fiub":  # float(v) of each element, vectorised
+            vals = dist.astype(np.float64)
+        else:
+            vals = np.asarray([float(v) for v in dist.tolist()], dtype=np.float64)
         ids = np.arange(vals.size, dtype=np.int64)
     elif isinstance(dist, dict):
         items = sorted(dist.items())

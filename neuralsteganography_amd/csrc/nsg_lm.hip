@@ -138,13 +138,15 @@ __host__ __device__ constexpr int k_chains(int K) { return K <= 1024 ? 1 : K <= 
 // nb = 4 / SK * blockIdx.x + w / SK, activation rows [16 * FM * blockIdx.y, +16 * FM) and chain w % SK; the
 // fragments come straight from global memory (small batches are latency- and weight-bandwidth-bound; an LDS
 // round trip would only add latency).  Chains meet in LDS and the chain-0 wave adds them in order.
-template <int FM, int SK, int EPI>
-__global__ __launch_bounds__(256) void gemm_direct(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
-                                                   int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy,
-                                                   int M, int N, int K) {
-    __shared__ f32x4 s_part[SK > 1 ? 4 : 1][SK > 1 ? FM : 1][64];
+template <int FM, int SK, int EPI, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_direct(const f16* __restrict__ X, int64_t ldx,
+                                                       const f16* __restrict__ Wt, int64_t ldw,
+                                                       const f16* __restrict__ bias, void* Y, int64_t ldy, int M, int N,
+                                                       int K) {
+    static_assert(NW % SK == 0, "a workgroup holds whole weight blocks");
+    __shared__ f32x4 s_part[SK > 1 ? NW : 1][SK > 1 ? FM : 1][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb = blockIdx.x * (4 / SK) + wave / SK;
+    const int nb = blockIdx.x * (NW / SK) + wave / SK;
     const int chain = wave % SK;
     const bool live = nb * 16 < N;  // uniform per wave; no early return: the chain hand-off has a barrier
     const int m0 = blockIdx.y * 16 * FM;
@@ -946,15 +948,15 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
 // issued before the normalisation so their latency hides it.  One launch per LN + GEMM pair instead of two: at
 // B = 1 the decode step is a chain of ~85 launch-latency-bound kernels.
 constexpr int LNG_MAXK = 1024;
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_direct_ln(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ lw,
-                                                      const f16* __restrict__ lb, float eps,
-                                                      const f16* __restrict__ Wt, int64_t ldw,
-                                                      const f16* __restrict__ bias, void* Y, int64_t ldy, int M, int N,
-                                                      int K) {
+template <int EPI, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_direct_ln(const f16* __restrict__ X, int64_t ldx,
+                                                          const f16* __restrict__ lw, const f16* __restrict__ lb,
+                                                          float eps, const f16* __restrict__ Wt, int64_t ldw,
+                                                          const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
+                                                          int N, int K) {
     __shared__ __attribute__((aligned(16))) f16 sA[16][LNG_MAXK + 8];  // +16 B per row: conflict-free b128 reads
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb = blockIdx.x * 4 + wave;
+    const int nb = blockIdx.x * NW + wave;
     const bool live = nb * 16 < N;
     const int r = lane & 15, c = lane >> 4;
     const int KS = K / 32;  // 32-wide k-steps
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(256) void gemm_direct_ln(const f16* __restrict__ X,
         }
     }
     const int NV4 = K >> 2;
-    for (int row = wave; row < M; row += 4) {
+    for (int row = wave; row < M; row += NW) {
         const f16* xr = X + (int64_t)row * ldx;
         float x[LN_MAXV][4];
 #pragma unroll
@@ -1040,14 +1042,19 @@ static bool persist_ok(int epi, const void* bias, int64_t ldy, int M, int N) {
            ((int64_t)M + 128) * ldy * esz < ((int64_t)1 << 31);
 }
 
+#ifndef NSG_DIRECT_NW
+#define NSG_DIRECT_NW 1  // waves per workgroup of the direct kernels when one chain per weight block (K <= 1024)
+#endif
+
 template <int FM, int EPI>
 static void launch_direct(const f16* x, int64_t ldx, const f16* wt, int64_t ldw, const f16* bias, void* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
     const int nbk = N / 16, my = (M + 16 * FM - 1) / (16 * FM);
+    constexpr int NW1 = NSG_DIRECT_NW;
     switch (k_chains(K)) {
         case 1:
-            hipLaunchKernelGGL((gemm_direct<FM, 1, EPI>), dim3((nbk + 3) / 4, my), dim3(256), 0, st, x, ldx, wt, ldw,
-                               bias, y, ldy, M, N, K);
+            hipLaunchKernelGGL((gemm_direct<FM, 1, EPI, NW1>), dim3((nbk + NW1 - 1) / NW1, my), dim3(64 * NW1), 0, st,
+                               x, ldx, wt, ldw, bias, y, ldy, M, N, K);
             break;
         case 2:
             hipLaunchKernelGGL((gemm_direct<FM, 2, EPI>), dim3((nbk + 1) / 2, my), dim3(256), 0, st, x, ldx, wt, ldw,
@@ -1216,22 +1223,23 @@ extern "C" int ns_lm_ln_gemm(const void* d_x, int64_t ldx, const void* d_lw, con
     const f16 *x = (const f16*)d_x, *wt = (const f16*)d_wt, *b = (const f16*)d_bias, *lw = (const f16*)d_lw,
               *lb = (const f16*)d_lb;
     const hipStream_t st = (hipStream_t)hip_stream;
-    const dim3 grid((N / 16 + 3) / 4);
+    constexpr int NW1 = NSG_DIRECT_NW;
+    const dim3 grid((N / 16 + NW1 - 1) / NW1), blk(64 * NW1);
     switch (epilogue) {
         case NS_LM_EPI_STORE:
-            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_STORE>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
+            hipLaunchKernelGGL((gemm_direct_ln<NS_LM_EPI_STORE, NW1>), grid, blk, 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
                                d_y, ldy, M, N, K);
             break;
         case NS_LM_EPI_GELU:
-            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_GELU>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
+            hipLaunchKernelGGL((gemm_direct_ln<NS_LM_EPI_GELU, NW1>), grid, blk, 0, st, x, ldx, lw, lb, eps, wt, ldw, b,
                                d_y, ldy, M, N, K);
             break;
         case NS_LM_EPI_RESIDUAL:
-            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_RESIDUAL>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt, ldw,
+            hipLaunchKernelGGL((gemm_direct_ln<NS_LM_EPI_RESIDUAL, NW1>), grid, blk, 0, st, x, ldx, lw, lb, eps, wt, ldw,
                                b, d_y, ldy, M, N, K);
             break;
         case NS_LM_EPI_STORE_F32:
-            hipLaunchKernelGGL(gemm_direct_ln<NS_LM_EPI_STORE_F32>, grid, dim3(256), 0, st, x, ldx, lw, lb, eps, wt,
+            hipLaunchKernelGGL((gemm_direct_ln<NS_LM_EPI_STORE_F32, NW1>), grid, blk, 0, st, x, ldx, lw, lb, eps, wt,
                                ldw, b, d_y, ldy, M, N, K);
             break;
         default: return NS_ERR_CONFIG;

@@ -1,7 +1,7 @@
 """CPU: the oracle's restatement of the reference's exact-rational coder (codec/arithmetic.py:234-550, row a12)
 reproduces every outcome of the reference run in tests/golden/fraction_golden.json -- tokens, per-token
 consumption, residual bit count, decoded bytes, and which call raises (mostly ArithmeticRangeError: the coder
-is non-functional for general payloads)."""
+is non-functional for general payloads; DESIGN.md §4, Fraction coder)."""
 
 import json
 from pathlib import Path
@@ -34,6 +34,7 @@ def test_fraction_coder_restatement_matches_reference(rec):
 
 
 def test_fraction_coder_is_mostly_non_functional():
-    """The documented reason a12 is not built: most payload cases end in ArithmeticRangeError."""
+    """The reference's coder cannot carry most payloads: most recorded cases end in ArithmeticRangeError
+    (the kernel of row a12 reproduces that, tests/test_gpu_fraction.py)."""
     failed = sum("encode_error" in r for r in G)
     assert failed >= len(G) // 3

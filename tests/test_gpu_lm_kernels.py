@@ -225,6 +225,13 @@ def test_decode_attention_is_batch_invariant(L0):
     out = torch.empty((B, H * D), device="cuda").half()
     assert f(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), B, H, D, L0,
              out.data_ptr(), out.stride(0), D ** -0.5, _stream_handle()) == 0
+    # a small batch (one-wave workgroups, partials merged across workgroups) twice in a row: same rows
+    for _ in range(2):
+        o80 = torch.empty((80, H * D), device="cuda").half()
+        assert f(qkv[300:].data_ptr(), qkv.stride(0), kc[300:].data_ptr(), vc[300:].data_ptr(), kc.stride(0),
+                 kc.stride(1), 80, H, D, L0, o80.data_ptr(), o80.stride(0), D ** -0.5, _stream_handle()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o80, out[300:380])
     for b in (0, 1, 399, 699):
         o1 = torch.empty((1, H * D), device="cuda").half()
         assert f(qkv[b:].data_ptr(), qkv.stride(0), kc[b:].data_ptr(), vc[b:].data_ptr(), kc.stride(0),
