@@ -75,6 +75,10 @@ def parse(argv=None):
     ap.add_argument("--optin-window", type=int, default=256,
                     help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-logits (PCIe-inclusive) side figure")
+    ap.add_argument("--no-fraction", action="store_true", help="skip the src Fraction-coder side line (row a12)")
+    ap.add_argument("--fraction-batch", type=int, default=1024)
+    ap.add_argument("--fraction-vocab", type=int, default=16)
+    ap.add_argument("--fraction-bytes", type=int, default=32)
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)
@@ -150,7 +154,76 @@ def cpu_baseline(args, seconds, streams_per_core=16):
             "sample": f"{cores} worker processes (1 thread each), each the reference's batch-1 token loop: HF "
                       f"GPT2LMHeadModel (random-init GPT-2-small, fp32, KV cache) + oracle or_encode_batch, "
                       f"{args.payload_bytes}-byte payloads, {dt:.1f} s; model construction excluded"}
+    if not args.no_fraction:
+        out["fraction_coder"] = _fraction_cpu(args)
     return out
+
+
+def _fraction_dists(V: int, n_steps: int, n_msgs: int):
+    """Per-step float64 distributions of the Fraction-coder leg: 97 random rows, message b's step t = row (b + t) % 97."""
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    base = rng.random((97, V))
+    base /= base.sum(axis=1, keepdims=True)
+    return [[base[(b + t) % 97] for t in range(n_steps)] for b in range(n_msgs)]
+
+
+def _fraction_cpu(args, seconds=4.0):
+    """The src Fraction coder's own arithmetic (fractions.Fraction, restated in oracle/fraction_coder.py) on one
+    core, over the fraction_coder leg's messages until ``seconds`` have passed."""
+    import time
+
+    from oracle import fraction_coder as fc
+
+    streams = _fraction_dists(args.fraction_vocab, 64, 256)
+    payload = bytes(args.fraction_bytes)
+    t0, tok, msgs = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < seconds and msgs < len(streams):
+        toks, _ = fc.encode(payload, streams[msgs])
+        tok += len(toks)
+        msgs += 1
+    dt = time.perf_counter() - t0
+    return {"value": 8 * args.fraction_bytes * msgs / dt, "unit": "payload bits/s", "cores": 1, "kind": "port",
+            "cover_tokens_per_s": tok / dt,
+            "sample": f"oracle/fraction_coder.py encode (fractions.Fraction), {msgs} messages of "
+                      f"{args.fraction_bytes} zero bytes over V = {args.fraction_vocab} rows, {dt:.1f} s"}
+
+
+def fraction_coder(args, rank, world, dev):
+    """Row a12, the src package's exact-rational coder (``codec/arithmetic.py:234-325``) as the device kernel:
+    ``--fraction-batch`` messages per GPU of ``--fraction-bytes`` zero bytes (the payloads this coder carries:
+    DESIGN.md §4) over per-step V-token float64 distributions, encoded in lockstep (timed, host-inclusive: the host
+    gathers each step's rows from the ProbDist iterables), then decoded and compared.  A side line."""
+    import torch
+    import torch.distributed as dist
+
+    from neuralsteganography_amd.codec import fraction as F
+    from neuralsteganography_amd.dist import reduce_job, shard_range
+
+    mine = shard_range(args.fraction_batch * world, world, rank)
+    streams = _fraction_dists(args.fraction_vocab, 64, len(mine))
+    payloads = [bytes(args.fraction_bytes)] * len(mine)
+    F.encode_bits_batch(payloads[:8], [iter(s) for s in streams[:8]], [{} for _ in range(8)])  # warm-up
+    states = [{} for _ in payloads]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    toks = F.encode_bits_batch(payloads, [iter(s) for s in streams], states)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    dec = F.decode_bits_batch(toks, [iter(s) for s in streams], [dict(st) for st in states])
+    ok = sum(d == p for d, p in zip(dec, payloads))
+    ntok = sum(len(t) for t in toks)
+    bits, tok, T, _ = reduce_job(8 * args.fraction_bytes * len(payloads), ntok, dt, 0.0, dev)
+    good = reduce_job(ok, 0, 0.0, 0.0, dev)[0]
+    return {"value": bits / T, "unit": "payload bits/s", "cover_tokens_per_s": tok / T, "seconds": T,
+            "messages": args.fraction_batch * world, "lockstep_steps": max(len(t) for t in toks),
+            "roundtrip_exact_fraction": good / (args.fraction_batch * world),
+            "workload": f"src Fraction coder (ns_frac_encode_step), {args.fraction_batch} messages/GPU x "
+                        f"{args.fraction_bytes} zero bytes, V = {args.fraction_vocab} float64 rows per step, "
+                        "host-inclusive lockstep encode"}
 
 
 def wide_path(args, rank, world, dev, steps=10, warmup=3):
@@ -581,6 +654,9 @@ def main():
     if not args.no_wide:
         log("wide path")
         side["wide_path"] = wide_path(args, rank, world, dev)
+    if not args.no_fraction:
+        log("src Fraction coder")
+        side["fraction_coder"] = fraction_coder(args, rank, world, dev)
     head = None
     if not args.no_e2e:
         # headline: config C3 end to end, encoded then decoded and checked
