@@ -239,6 +239,40 @@ def _stats_rows(acc: np.ndarray, bits_consumed: Optional[np.ndarray] = None) -> 
     return out
 
 
+def _bit_array(bits) -> np.ndarray:
+    """A payload bit list as uint8 (nonzero = 1 after packing).  Python lists go through ``bytes`` (one C pass,
+    ≈3x faster than numpy's per-object conversion: 4,096 KiB-payload lists are ≈1 s of host time otherwise)."""
+    if isinstance(bits, (list, tuple)):
+        try:
+            return np.frombuffer(bytes(bits), dtype=np.uint8)
+        except (ValueError, TypeError):
+            pass
+    return np.asarray(bits, dtype=np.uint8)
+
+
+def _rows_to_lists(dev_rows, lengths) -> List[List[int]]:
+    """Row i's first lengths[i] entries of a device [B, cap] int array as Python int lists: only the columns in
+    use cross PCIe (the history buffer is sized for the KV budget, far wider than a finished job's tokens), and
+    the rows become lists in one conversion."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    n = int(lengths.max(initial=0))
+    if n == 0:
+        return [[] for _ in range(dev_rows.shape[0])]
+    rows = dev_rows[:, :n].cpu().numpy().tolist()
+    return [r[:k] if k < n else r for r, k in zip(rows, lengths.tolist())]
+
+
+def _bit_rows_to_lists(dev_bytes, nbits) -> List[List[int]]:
+    """Row i's first nbits[i] bits (LSB-first bytes on the device) as Python int lists."""
+    nbits = np.asarray(nbits, dtype=np.int64)
+    nb = int(nbits.max(initial=0))
+    if nb == 0:
+        return [[] for _ in range(dev_bytes.shape[0])]
+    host = dev_bytes[:, : (nb + 7) // 8].cpu().numpy()
+    rows = np.unpackbits(host, axis=1, bitorder="little")[:, :nb].tolist()
+    return [r[:k] if k < nb else r for r, k in zip(rows, nbits.tolist())]
+
+
 class EncodeSession:
     """B streams being encoded; call :meth:`step` once per generated token with that step's logits.
 
@@ -259,7 +293,7 @@ class EncodeSession:
         pl = np.zeros((self.B, stride), dtype=np.uint8)
         for i, bits in enumerate(payload_bits):
             if len(bits):
-                packed = np.packbits(np.asarray(bits, dtype=np.uint8), bitorder="little")
+                packed = np.packbits(_bit_array(bits), bitorder="little")
                 pl[i, : packed.size] = packed
         self.payload = torch.from_numpy(pl).to(dev)
         self.nbits = torch.from_numpy(self.nbits_host).to(dev)
@@ -346,8 +380,7 @@ class EncodeSession:
         f = self.fields()
         if int(f["ntokens"].max(initial=0)) > self.hist.shape[1]:
             raise ConfigurationError("token history overflow: raise max_tokens")
-        h = self.hist.cpu().numpy()
-        return [h[i, : int(f["ntokens"][i])].astype(np.int64).tolist() for i in range(self.B)]
+        return _rows_to_lists(self.hist, f["ntokens"])
 
     def trace_rows(self) -> np.ndarray:
         """Last-step trace as a structured host array (k, kprime, sel, n, token, exact, S)."""
@@ -437,12 +470,7 @@ class DecodeSession:
         bad = np.nonzero(f["flags"] & _lib.NS_ST_ERR_DIVERGE)[0]
         if bad.size:
             raise DecodeDivergenceError(f"streams {bad.tolist()[:8]}: received token outside the kept top-k")
-        ob = self.out_bits.cpu().numpy()
-        out = []
-        for i in range(self.B):
-            nb = int(f["bit_pos"][i])
-            out.append(np.unpackbits(ob[i], bitorder="little")[:nb].astype(np.int64).tolist())
-        return out
+        return _bit_rows_to_lists(self.out_bits, f["bit_pos"])
 
 
 def encode_batch(ctx: CoderContext, payload_bits: Sequence[Sequence[int]], logits_fn, *, max_steps: int = 1 << 20,
@@ -524,9 +552,8 @@ class SampleSession:
         return np.rec.fromarrays([t[:, 0], t[:, 1], t[:, 2], t[:, 3], t[:, 4]], names="k,kprime,sel,n,token")
 
     def tokens(self) -> List[List[int]]:
-        h = self.hist.cpu().numpy()
         n = min(self.steps, self.hist.shape[1])
-        return [h[i, :n].astype(np.int64).tolist() for i in range(self.B)]
+        return _rows_to_lists(self.hist, np.full(self.B, n))
 
     def stats(self) -> List[dict]:
         if self.stats_acc is None:
@@ -614,9 +641,7 @@ class StreamingDecodeSession:
 
     def bits(self) -> List[List[int]]:
         f = _state_fields(self.state)
-        ob = self.out_bits.cpu().numpy()
-        return [np.unpackbits(ob[i], bitorder="little")[: int(f["bit_pos"][i])].astype(np.int64).tolist()
-                for i in range(self.B)]
+        return _bit_rows_to_lists(self.out_bits, f["bit_pos"])
 
 
 def rank_quality(quality) -> "_lib.NsRankQuality":
