@@ -188,3 +188,19 @@ def test_fraction_reference_error_behaviour(F):
     st = {}
     assert F.encode_bits(b"", iter([]), state=st) == [] and st == {"history": (), "residual_bits": bytes(8)}
     assert F.decode_bits([], iter([])) == b""
+
+
+def test_fraction_table_growth_and_capacity(F):
+    """A 300-token step needs a cumulative table beyond the default 65,536 limbs (the lcm of 300 random 30-bit
+    denominators): the step re-runs with a larger table and still matches the restatement; a tiny interval
+    arena raises FractionCapacityError instead of writing past it."""
+    rng = np.random.default_rng(4)
+    p = rng.random(300)
+    ds = [p / p.sum()]
+    st = {}
+    toks = F.encode_bits(b"\x00", iter(ds), state=st)
+    want, wst = fc.encode(b"\x00", ds)
+    assert toks == want and tuple(st["history"]) == tuple(wst["history"])
+    assert F.decode_bits(toks, iter(ds), state=dict(st)) == b"\x00"
+    with pytest.raises(F.FractionCapacityError):
+        F.encode_bits_batch([bytes(8)], [iter(dists(16, 1016))], cap_limbs=8)
