@@ -32,6 +32,19 @@ namespace nsg {
 
 constexpr int ATT_D = 64;
 
+#ifndef NSG_ATT_LOAD
+#define NSG_ATT_LOAD 0  // K/V row loads: 0 = non-temporal (the rows are not reused within the step), 1 = default policy
+#endif
+
+template <class R>
+__device__ __forceinline__ R att_load(const R* p) {
+#if NSG_ATT_LOAD == 1
+    return *p;
+#else
+    return __builtin_nontemporal_load(p);
+#endif
+}
+
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -230,13 +243,13 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                         const bool pre = row < T0;
                         const E* ka = pre ? kpb + (int64_t)row * ATT_D : kb + soff(row);
                         const E* va = pre ? vpb + (int64_t)row * ATT_D : vb + soff(row);
-                        kr[u] = __builtin_nontemporal_load((const Raw*)ka);
-                        vr[u] = __builtin_nontemporal_load((const Raw*)va);
+                        kr[u] = att_load((const Raw*)ka);
+                        vr[u] = att_load((const Raw*)va);
                     } else {
                         const int row = j0 + RPI * u + g;
                         const int64_t o = soff(row);
-                        kr[u] = __builtin_nontemporal_load((const Raw*)(kb + o));
-                        vr[u] = __builtin_nontemporal_load((const Raw*)(vb + o));
+                        kr[u] = att_load((const Raw*)(kb + o));
+                        vr[u] = att_load((const Raw*)(vb + o));
                     }
                 }
             };
