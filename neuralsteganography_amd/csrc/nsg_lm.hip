@@ -1152,10 +1152,14 @@ static int auto_cfg(int M, int N, int K) {
     const bool split = k_chains(K) > 1;
     if (M <= 16) return (N >= 8192 && !split) ? CFG_T64_2 : CFG_DIRECT16;
     if (split && M <= 256) return M <= 64 ? CFG_DIRECT16 : M <= 128 ? CFG_DIRECT32 : CFG_DIRECT64;
-    if (N >= 8192 && M >= 512) return CFG_T128_2;
+    // the vocabulary-wide head: 256 x 256 ping-pong tiles below B = 2048 (GPT-2-medium B = 1024: 786 vs 740
+    // TFLOP/s), 128 x 128 above (B = 4096: 752 vs 726; profiles/r04/lmprobe_r04aa_*.jsonl)
+    if (N >= 8192 && M >= 512) return (!split && M < 2048) ? CFG_PP256 : CFG_T128_2;
     // GPT-2's c_fc at B >= 4096 (profiles/lmprobe_r03o_b4096.jsonl: 581 vs 501 TFLOP/s for the 64 x 64 tiles);
-    // c_attn (N = 2304) and the smaller batches stay on the 64 x 64 tiles (more tiles than CUs)
+    // GPT-2-medium's c_fc (N = 4096) at B = 1024 on 128 x 64 tiles (506 vs 471); c_attn (N = 2304 / 3072) and the
+    // smaller batches stay on the 64 x 64 tiles (more tiles than CUs)
     if (!split && M >= 4096 && N >= 2560) return CFG_PP256;
+    if (!split && M >= 1024 && N >= 4096) return CFG_T128x64_3;
     return CFG_T64_2;
 }
 
