@@ -48,7 +48,8 @@ int ns_frac_init(ns_frac_ctx* ctx, int B, const int64_t* h_nbits, void* hip_stre
  *   reference's order (array: 0..V-1; dict: sorted keys), d_count[b] = V entries (<= ld);
  *   d_bits [B, bits_stride] the payload, one bit per byte, MSB-first (zero-padded past the payload by the step);
  *   table_limbs: per-stream room for the V + 1 cumulative numerators (NS_FRAC_ERR_CAPACITY if short);
- *   max_bits: the largest payload length of the batch (sizes the scratch).
+ *   max_bits: the largest payload length of the batch (sizes the scratch; at most 2^20 -- NS_ERR_CONFIG above: a
+ *   failing step searches one depth per payload bit, each linear in the integers' growing size).
  * Outputs d_token[b] (the token id), d_used[b] (bits consumed = the depth, the reference's history entry). */
 int ns_frac_encode_step(ns_frac_ctx* ctx, int B, const double* d_probs, const int32_t* d_ids, int64_t ld,
                         const int32_t* d_count, const uint8_t* d_bits, int64_t bits_stride, int64_t max_bits,

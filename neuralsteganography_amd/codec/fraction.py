@@ -30,6 +30,8 @@ NS_FRAC_ERR_CAPACITY = -5
 DEFAULT_CAP_LIMBS = 4096          # 131,072-bit interval integers per stream
 DEFAULT_TABLE_LIMBS = 1 << 16     # cumulative numerators of one step, grown x8 on demand ...
 MAX_TABLE_LIMBS = 1 << 24         # ... up to 64 MiB per stream
+MAX_PAYLOAD_BITS = 1 << 16        # payloads above 8 KiB (and consumption entries above this + 64) are refused: a
+#                                   failing step searches one depth per payload bit on ever longer integers
 _INT32 = (-(1 << 31), (1 << 31) - 1)
 
 
@@ -160,17 +162,22 @@ def encode_bits_batch(payloads: Sequence[bytes], probs: Sequence[Iterable], stat
     out: list = [[] for _ in range(B)]
     used_hist: List[List[int]] = [[] for _ in range(B)]
     err: list = [None] * B
-    live = [i for i in range(B) if n[i] > 0]
+    for i in range(B):
+        if n[i] > MAX_PAYLOAD_BITS:
+            err[i] = FractionCapacityError(f"payload of {int(n[i])} bits: the device Fraction coder takes at most "
+                                           f"{MAX_PAYLOAD_BITS} bits per message")
+    live = [i for i in range(B) if n[i] > 0 and err[i] is None]
     if live:
         dv = _Device(B, cap_limbs, device)
         torch = dv.torch
         try:
-            stride = max(1, int(n.max()))
+            stride = max(1, max(int(n[i]) for i in live))
             host_bits = np.zeros((B, stride), dtype=np.uint8)
-            for i, b in enumerate(bits):
-                host_bits[i, :len(b)] = b
+            for i in live:
+                host_bits[i, :len(bits[i])] = bits[i]
             d_bits = torch.from_numpy(host_bits).to(dv.dev)
-            dv.check(dv.L.ns_frac_init(dv.ctx, B, n.ctypes.data, dv.stream()), "ns_frac_init")
+            n_live = np.where([err[i] is None for i in range(B)], n, 0).astype(np.int64)
+            dv.check(dv.L.ns_frac_init(dv.ctx, B, n_live.ctypes.data, dv.stream()), "ns_frac_init")
             token = torch.empty(B, dtype=torch.int32, device=dv.dev)
             used = torch.empty(B, dtype=torch.int32, device=dv.dev)
             status = torch.empty(B, dtype=torch.int32, device=dv.dev)
@@ -255,6 +262,10 @@ def decode_bits_batch(token_lists: Sequence[Sequence[int]], probs: Sequence[Iter
             err[i] = DecodeDivergenceError("Bit consumption history is required for decoding")
             continue
         cons[i] = [int(c) for c in history[:len(toks[i])]]
+        if max(cons[i]) > MAX_PAYLOAD_BITS + 64:
+            err[i] = FractionCapacityError(f"a token consuming {max(cons[i])} bits: the device Fraction coder takes at "
+                                           f"most {MAX_PAYLOAD_BITS + 64} per token")
+            continue
         live.append(i)
     written = np.zeros(B, dtype=np.int64)
     if live:

@@ -465,7 +465,9 @@ extern "C" int ns_frac_init(ns_frac_ctx* ctx, int B, const int64_t* h_nbits, voi
 // per-stream scratch: fractions (4 limbs per entry), D, NTMP temporaries, the cumulative table
 static int frac_prepare(ns_frac_ctx* ctx, int B, int64_t ld, int64_t max_bits, int64_t table_limbs, hipStream_t s,
                         nsg::frac::Args& a) {
-    if (B <= 0 || B > ctx->max_batch || ld < 0 || ld > (1 << 28) || max_bits < 0 || max_bits > ((int64_t)1 << 34) ||
+    // max_bits bounds lane 0's depth search (one iteration per payload bit a failing step tries, each linear in
+    // the integers' size, which grows by a bit per depth): 2^20 keeps the worst step of a stream to seconds
+    if (B <= 0 || B > ctx->max_batch || ld < 0 || ld > (1 << 28) || max_bits < 0 || max_bits > ((int64_t)1 << 20) ||
         table_limbs < 2 || table_limbs > ((int64_t)1 << 30))
         return frac_fail(ctx, "ns_frac step: bad sizes", NS_ERR_CONFIG);
     const int64_t tmp = 2 * (int64_t)ctx->cap + (max_bits + 64) / 32 + 8;

@@ -204,3 +204,11 @@ def test_fraction_table_growth_and_capacity(F):
     assert F.decode_bits(toks, iter(ds), state=dict(st)) == b"\x00"
     with pytest.raises(F.FractionCapacityError):
         F.encode_bits_batch([bytes(8)], [iter(dists(16, 1016))], cap_limbs=8)
+
+
+def test_fraction_payload_bound(F):
+    """Payloads beyond the device coder's bound raise FractionCapacityError for that message only."""
+    got = F.encode_bits_batch([bytes(F.MAX_PAYLOAD_BITS // 8 + 1), b"\x00"],
+                              [iter(dists(4, 1004)), iter(dists(4, 1004))], [{}, {}], return_exceptions=True)
+    assert isinstance(got[0], F.FractionCapacityError)
+    assert got[1] == fc.encode(b"\x00", dists(4, 1004))[0]
