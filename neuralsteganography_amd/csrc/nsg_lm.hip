@@ -716,11 +716,15 @@ __global__ __launch_bounds__(512) void gemm_big(const f16* __restrict__ X, int64
 // every M slot with vmcnt(0) (its copies of t + 1 have landed): K-tile t+1 goes into the buffer last read in slot
 // 2t (group 1's L(t-1)), and is read from slot 2t+3 (group 0) / 2t+4 (group 1) on, after the barriers that follow
 // its writers' waits.  One K chain (K <= 1024); ragged N / M clamped on load, not stored.
-template <int EPI>
+// BN = 192 (FN = 3): the same kernel with 48 weight rows per wave -- GPT-2's c_fc at B = 4,096 is then 16 x 16 =
+// 256 tiles, one per CU, where 256-wide panels leave a quarter of the CUs idle (192 tiles).
+template <int EPI, int BN = 256>
 __global__ __launch_bounds__(512) void gemm_pp(const f16* __restrict__ X, int64_t ldx, const f16* __restrict__ Wt,
                                                int64_t ldw, const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
                                                int N, int K) {
-    constexpr int BN = 256, BM = 256, FN = 4, FM = 8, SB = (BN + BM) * 128;
+    static_assert(BN == 256 || BN == 192, "weight panel");
+    constexpr int BM = 256, FN = BN / 64, FM = 8, SB = (BN + BM) * 128;
+    constexpr int WP = BN / 32;  // weight pieces (32 rows each) staged by group 0
     __shared__ __attribute__((aligned(16))) char smem[2 * SB];
 
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -747,9 +751,9 @@ __global__ __launch_bounds__(512) void gemm_pp(const f16* __restrict__ X, int64_
         asm volatile("" : "+v"(r8));
         if (g == 0) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                const f16* p = q < 8 ? Wt + (int64_t)min(n0 + q * 32 + r8, N - 1) * ldw
-                                     : X + (int64_t)min(m0 + (q - 8) * 32 + r8, M - 1) * ldx;
+            for (int q = 0; q < WP + 4; ++q) {
+                const f16* p = q < WP ? Wt + (int64_t)min(n0 + q * 32 + r8, N - 1) * ldw
+                                      : X + (int64_t)min(m0 + (q - WP) * 32 + r8, M - 1) * ldx;
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + chunk * 8 + kt * BK),
                                                  (__attribute__((address_space(3))) void*)(dst + (q * 4 + wn) * 1024),
                                                  16, 0, 0);
@@ -759,7 +763,7 @@ __global__ __launch_bounds__(512) void gemm_pp(const f16* __restrict__ X, int64_
             for (int q = 0; q < 4; ++q) {
                 const f16* p = X + (int64_t)min(m0 + 128 + q * 32 + r8, M - 1) * ldx;
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + chunk * 8 + kt * BK),
-                                                 (__attribute__((address_space(3))) void*)(dst + (48 + q * 4 + wn) * 1024),
+                                                 (__attribute__((address_space(3))) void*)(dst + ((BN + 128) / 8 + q * 4 + wn) * 1024),
                                                  16, 0, 0);
             }
         }
@@ -1019,6 +1023,7 @@ enum GemmCfg {
     CFG_B256,                                         // 256 x 256, 8 waves of 64 x 128 (K <= 1024)
     CFG_P128_2, CFG_P128_3, CFG_P128_4,               // persistent 128 x 128, 2 / 3 / 4 stages (2 / 1 / 1 per CU)
     CFG_PP256,                                        // 256 x 256, two ping-pong wave groups (K <= 1024)
+    CFG_PP192,                                        // 192 weight rows x 256, the same ping-pong kernel
     CFG_COUNT
 };
 
@@ -1110,6 +1115,14 @@ static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_
                                    N, K);
             }
             break;
+        case CFG_PP192:
+            if (split) {
+                NSG_TILED(128, 128, 2, 2, 2);
+            } else {
+                hipLaunchKernelGGL((gemm_pp<EPI, 192>), tiles(192, 256), dim3(512), 0, st, x, ldx, wt, ldw, bias, y,
+                                   ldy, M, N, K);
+            }
+            break;
         case CFG_P128_2:
         case CFG_P128_3:
         case CFG_P128_4: {
@@ -1155,10 +1168,16 @@ static int auto_cfg(int M, int N, int K) {
     // the vocabulary-wide head: 256 x 256 ping-pong tiles below B = 2048 (GPT-2-medium B = 1024: 786 vs 740
     // TFLOP/s), 128 x 128 above (B = 4096: 752 vs 726; profiles/r04/lmprobe_r04aa_*.jsonl)
     if (N >= 8192 && M >= 512) return (!split && M < 2048) ? CFG_PP256 : CFG_T128_2;
-    // GPT-2's c_fc at B >= 4096 (profiles/lmprobe_r03o_b4096.jsonl: 581 vs 501 TFLOP/s for the 64 x 64 tiles);
-    // GPT-2-medium's c_fc (N = 4096) at B = 1024 on 128 x 64 tiles (506 vs 471); c_attn (N = 2304 / 3072) and the
-    // smaller batches stay on the 64 x 64 tiles (more tiles than CUs)
-    if (!split && M >= 4096 && N >= 2560) return CFG_PP256;
+    // B >= 4096, K <= 1024, wide N: the ping-pong kernel, with 192- or 256-wide weight panels, whichever needs fewer
+    // panel-rows of work per CU (GPT-2's c_fc: 256 tiles of 192 = one per CU, 644 vs 579 TFLOP/s for 192 tiles of
+    // 256; c_attn 556 vs 487 on 64 x 64 tiles; profiles/r04/lmprobe_r04ag_*.jsonl).  GPT-2-medium's c_fc (N = 4096)
+    // at B = 1024 on 128 x 64 tiles (506 vs 471); the other shapes and smaller batches stay on 64 x 64 tiles.
+    if (!split && M >= 4096 && N >= 2048) {
+        const long cu = cu_count(), tm = (M + 255) / 256;
+        const long w256 = (tm * ((N + 255) / 256) + cu - 1) / cu * 256;
+        const long w192 = (tm * ((N + 191) / 192) + cu - 1) / cu * 192;
+        return w192 < w256 ? CFG_PP192 : CFG_PP256;
+    }
     if (!split && M >= 1024 && N >= 4096) return CFG_T128x64_3;
     return CFG_T64_2;
 }
