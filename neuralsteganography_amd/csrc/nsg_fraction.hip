@@ -438,10 +438,10 @@ extern "C" ns_frac_ctx* ns_frac_create(int max_batch, int cap_limbs, int device)
 
 extern "C" void ns_frac_destroy(ns_frac_ctx* ctx) {
     if (!ctx) return;
-    hipFree(ctx->st);
-    hipFree(ctx->state);
-    hipFree(ctx->nbits);
-    hipFree(ctx->scratch);
+    (void)hipFree(ctx->st);
+    (void)hipFree(ctx->state);
+    (void)hipFree(ctx->nbits);
+    (void)hipFree(ctx->scratch);
     delete ctx;
 }
 
@@ -475,8 +475,8 @@ static int frac_prepare(ns_frac_ctx* ctx, int B, int64_t ld, int64_t max_bits, i
     stride += stride & 1;  // 8-byte alignment of the next stream's fraction numerators
     const size_t bytes = sizeof(limb) * (size_t)stride * B;
     if (bytes > ctx->scratch_bytes) {
-        hipStreamSynchronize(s);
-        hipFree(ctx->scratch);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(ctx->scratch);
         ctx->scratch = nullptr;
         ctx->scratch_bytes = 0;
         if (hipMalloc(&ctx->scratch, bytes) != hipSuccess)
