@@ -14,7 +14,15 @@
  * iterating the ProbDist iterables, type / sign / NaN checks, the state dict and the exceptions.
  *
  * Status per stream (d_status) after a step: NS_FRAC_OK, NS_FRAC_SKIPPED (no work for this stream), or an
- * error -- the state is left unchanged on every error, so a step can be re-run with a larger table.
+ * error -- the state is left unchanged on every error, so a step can be re-run with a larger table.  A skipped
+ * stream's d_token / d_used entries are not written, so streams can be run in several launches that share the
+ * output buffers (e.g. a re-run of the NS_FRAC_ERR_TABLE streams only).
+ *
+ * Supported envelope: D = lcm of a step's limit_denominator(2^30) denominators must fit cap_limbs 32-bit limbs;
+ * V unrelated 30-bit denominators make D about 30 V bits, so with the default 4,096 limbs a step holds up to
+ * ~4,000 entries with unrelated denominators (dyadic / shared denominators cost nothing), and the interval
+ * integers grow by about the size of D per token.  Real GPT-2 rows (V = 50,257) exceed it on the first step
+ * (NS_FRAC_ERR_CAPACITY): that is the reference's own arithmetic, whose fractions grow the same way.
  */
 #ifndef NSG_FRACTION_H
 #define NSG_FRACTION_H
@@ -33,7 +41,9 @@ typedef struct ns_frac_ctx ns_frac_ctx;
 #define NS_FRAC_ERR_UNRESOLVED (-2)  /* "Unable to resolve token interval with available bits" (:434-435)      */
 #define NS_FRAC_ERR_NOT_PRESENT (-3) /* "Token {id} not present in distribution" (:460-461)                    */
 #define NS_FRAC_ERR_NO_PREFIX (-4)   /* "No binary prefix fits within the interval" (:531-532)                 */
-#define NS_FRAC_ERR_CAPACITY (-5)    /* an integer outgrew cap_limbs, or the cumulative table table_limbs      */
+#define NS_FRAC_ERR_CAPACITY (-5)    /* an integer outgrew cap_limbs (no larger table can help)               */
+#define NS_FRAC_ERR_TABLE (-6)       /* the step's cumulative table needs more than table_limbs per stream:
+                                        re-run that stream with a larger table (its state is unchanged)       */
 
 /* Context for up to max_batch streams whose interval integers may grow to cap_limbs 32-bit limbs each. */
 ns_frac_ctx* ns_frac_create(int max_batch, int cap_limbs, int device);
@@ -42,6 +52,14 @@ const char* ns_frac_last_error(const ns_frac_ctx* ctx);
 
 /* Start B streams: [lo, hi) = [0, 1), nothing consumed; h_nbits[b] = payload bits of stream b (host array). */
 int ns_frac_init(ns_frac_ctx* ctx, int B, const int64_t* h_nbits, void* hip_stream);
+
+/* Scratch slots: with d_slot set (device int32[B], until reset with NULL), stream b uses scratch slot d_slot[b]
+ * (< nslots) and a stream whose slot is negative is skipped, so a launch that runs R of B streams needs scratch
+ * for R streams only.  d_slot must stay valid while steps run.  Default (NULL): slot b for stream b. */
+int ns_frac_set_slots(ns_frac_ctx* ctx, const int32_t* d_slot, int nslots);
+
+/* Device scratch bytes one step allocates for nslots streams (the context keeps the largest so far). */
+int64_t ns_frac_scratch_bytes(const ns_frac_ctx* ctx, int nslots, int64_t ld, int64_t max_bits, int64_t table_limbs);
 
 /* One encode step for every stream b with d_count[b] >= 0 and payload bits left (else NS_FRAC_SKIPPED):
  *   d_probs [B, ld] float64 values and d_ids [B, ld] int32 token ids of the stream's distribution in the

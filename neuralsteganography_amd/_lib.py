@@ -34,7 +34,7 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
            "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm",
            "ns_frac_create", "ns_frac_destroy", "ns_frac_last_error", "ns_frac_init", "ns_frac_encode_step",
-           "ns_frac_decode_step")
+           "ns_frac_decode_step", "ns_frac_set_slots", "ns_frac_scratch_bytes")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
 
 
@@ -167,6 +167,10 @@ def lib() -> ctypes.CDLL:
     L.ns_frac_encode_step.argtypes = [vp, ci, vp, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, vp]
     L.ns_frac_decode_step.restype = ci
     L.ns_frac_decode_step.argtypes = [vp, ci, vp, vp, i64, vp, vp, vp, i64, i64, vp, i64, vp, vp, vp]
+    L.ns_frac_set_slots.restype = ci
+    L.ns_frac_set_slots.argtypes = [vp, vp, ci]
+    L.ns_frac_scratch_bytes.restype = i64
+    L.ns_frac_scratch_bytes.argtypes = [vp, ci, i64, i64, i64]
     _lib = L
     return L
 

@@ -25,11 +25,12 @@ from .errors import ArithmeticRangeError, DecodeDivergenceError
 
 NS_FRAC_OK, NS_FRAC_SKIPPED = 0, 1
 NS_FRAC_ERR_NO_MASS, NS_FRAC_ERR_UNRESOLVED, NS_FRAC_ERR_NOT_PRESENT, NS_FRAC_ERR_NO_PREFIX = -1, -2, -3, -4
-NS_FRAC_ERR_CAPACITY = -5
+NS_FRAC_ERR_CAPACITY, NS_FRAC_ERR_TABLE = -5, -6
 
 DEFAULT_CAP_LIMBS = 4096          # 131,072-bit interval integers per stream
 DEFAULT_TABLE_LIMBS = 1 << 16     # cumulative numerators of one step, grown x8 on demand ...
 MAX_TABLE_LIMBS = 1 << 24         # ... up to 64 MiB per stream
+SCRATCH_BUDGET_BYTES = 8 << 30    # device scratch of one launch; a larger table than this allows fails the message
 MAX_PAYLOAD_BITS = 1 << 16        # payloads above 8 KiB (and consumption entries above this + 64) are refused: a
 #                                   failing step searches one depth per payload bit on ever longer integers
 _INT32 = (-(1 << 31), (1 << 31) - 1)
@@ -93,7 +94,7 @@ class _Device:
         self.ctx = self.L.ns_frac_create(B, int(cap_limbs), self.dev.index or 0)
         if not self.ctx:
             raise RuntimeError("ns_frac_create failed: " + self.L.ns_frac_last_error(None).decode())
-        self.table = DEFAULT_TABLE_LIMBS
+        self.tables = np.full(B, DEFAULT_TABLE_LIMBS, dtype=np.int64)  # per stream: grown only where a step needs it
 
     def close(self) -> None:
         if self.ctx:
@@ -126,22 +127,39 @@ class _Device:
             count[i] = len(vals)
         return (torch.from_numpy(probs).to(self.dev), torch.from_numpy(ids).to(self.dev), count, ld)
 
-    def run(self, launch, count: np.ndarray, status_dev) -> np.ndarray:
-        """Launch with the given counts; re-run the streams that ran out of table room with a larger table
-        (a failed stream's state is unchanged).  Returns the per-stream status."""
+    def run(self, launch, count: np.ndarray, status_dev, ld: int, max_bits: int, collect) -> np.ndarray:
+        """Run the step for the streams with ``count >= 0``: one launch per table size in use, each with scratch
+        for its own streams only (``ns_frac_set_slots``).  A stream whose step needs a larger cumulative table
+        (``NS_FRAC_ERR_TABLE``; its state is unchanged) re-runs with 8x the table -- kept for its later steps --
+        until ``MAX_TABLE_LIMBS`` or the scratch budget, past which it fails with ``NS_FRAC_ERR_CAPACITY``.
+        ``collect(mask)`` reads the per-stream outputs of the streams that ran in a launch before the next one.
+        Returns the per-stream status."""
         torch = self.torch
         status = np.full(self.B, NS_FRAC_SKIPPED, dtype=np.int32)
-        todo = count.copy()
-        while True:
-            launch(torch.from_numpy(todo).to(self.dev), self.table)
-            st = status_dev.cpu().numpy()
-            ran = todo >= 0
-            status[ran] = st[ran]
-            short = ran & (st == NS_FRAC_ERR_CAPACITY)
-            if not short.any() or self.table >= MAX_TABLE_LIMBS:
-                return status
-            self.table = min(self.table * 8, MAX_TABLE_LIMBS)
-            todo = np.where(short, count, -1).astype(np.int32)
+        pending = count >= 0
+        while pending.any():
+            table = int(self.tables[pending].min())
+            grp = pending & (self.tables == table)
+            pending &= ~grp
+            n = int(grp.sum())
+            if self.L.ns_frac_scratch_bytes(self.ctx, n, ld, max_bits, table) > SCRATCH_BUDGET_BYTES:
+                status[grp] = NS_FRAC_ERR_CAPACITY
+                continue
+            d_slot = torch.from_numpy(np.where(grp, np.cumsum(grp) - 1, -1).astype(np.int32)).to(self.dev)
+            self.check(self.L.ns_frac_set_slots(self.ctx, d_slot.data_ptr(), n), "ns_frac_set_slots")
+            try:
+                launch(torch.from_numpy(np.where(grp, count, -1).astype(np.int32)).to(self.dev), table)
+                st = status_dev.cpu().numpy()  # synchronises: d_slot is no longer read
+            finally:
+                self.check(self.L.ns_frac_set_slots(self.ctx, None, 0), "ns_frac_set_slots")
+            collect(grp)
+            status[grp] = st[grp]
+            short = grp & (st == NS_FRAC_ERR_TABLE)
+            grow = short & (self.tables < MAX_TABLE_LIMBS)
+            status[short & ~grow] = NS_FRAC_ERR_CAPACITY
+            self.tables[grow] = np.minimum(self.tables[grow] * 8, MAX_TABLE_LIMBS)
+            pending |= grow
+        return status
 
 
 def _capacity_error() -> FractionCapacityError:
@@ -181,6 +199,13 @@ def encode_bits_batch(payloads: Sequence[bytes], probs: Sequence[Iterable], stat
             token = torch.empty(B, dtype=torch.int32, device=dv.dev)
             used = torch.empty(B, dtype=torch.int32, device=dv.dev)
             status = torch.empty(B, dtype=torch.int32, device=dv.dev)
+            tok = np.full(B, -1, dtype=np.int32)
+            use = np.zeros(B, dtype=np.int32)
+
+            def collect(mask):
+                tok[mask] = token.cpu().numpy()[mask]
+                use[mask] = used.cpu().numpy()[mask]
+
             its = [iter(p) for p in probs]
             pos = np.zeros(B, dtype=np.int64)
             while live:
@@ -206,8 +231,7 @@ def encode_bits_batch(payloads: Sequence[bytes], probs: Sequence[Iterable], stat
                                                       token.data_ptr(), used.data_ptr(), status.data_ptr(),
                                                       dv.stream()), "ns_frac_encode_step")
 
-                st = dv.run(launch, count, status)
-                tok, use = token.cpu().numpy(), used.cpu().numpy()
+                st = dv.run(launch, count, status, ld, stride, collect)
                 for i in list(live):
                     s = int(st[i])
                     if s == NS_FRAC_OK:
@@ -315,7 +339,7 @@ def decode_bits_batch(token_lists: Sequence[Sequence[int]], probs: Sequence[Iter
                                                       d_pos.data_ptr(), status.data_ptr(), dv.stream()),
                              "ns_frac_decode_step")
 
-                st = dv.run(launch, count, status)
+                st = dv.run(launch, count, status, ld, max_used, lambda mask: None)
                 for i in list(live):
                     s = int(st[i])
                     if s == NS_FRAC_OK:

@@ -198,6 +198,10 @@ def _rank_rows(ctx: "CoderContext", B: int, rows, q):
     :class:`~neuralsteganography_amd.codec.distribution.ProbRows` registered with ``ns_set_rank_rows`` (the
     reference's quality errors raised on the host first)."""
     if not getattr(rows, "prob_rows", False):
+        if ctx.params.dtype == "f64":
+            # an f64 context reads rk_count / rk_idmap registered for ProbRows: a plain matrix would leave it reading
+            # an earlier step's (possibly freed) tensors (ADVICE r4)
+            raise ConfigurationError("a coder context of dtype 'f64' takes provider ProbRows only")
         _check_logits(ctx, B, rows)
         return rows
     if ctx.params.dtype != "f64":

@@ -75,6 +75,8 @@ struct Args {
     int32_t* token_out;  // encode
     int32_t* used_out;
     int32_t* status;
+    const int32_t* slot;  // scratch slot of stream b (ns_frac_set_slots), or null: slot b
+    int64_t nslots;       // scratch slots allocated
 };
 
 // dst += src over n limbs, every lane of the wave taking one limb per 64-limb chunk.  Carries between lanes:
@@ -241,23 +243,18 @@ __global__ __launch_bounds__(64) void frac_step_kernel(Args a) {
     __shared__ int s_nd, s_sw, s_err;
     Stream& st = a.st[b];
     const int V = a.count[b];
-    bool skip = V < 0;
+    const int64_t slot = a.slot ? (int64_t)a.slot[b] : (int64_t)b;
+    bool skip = V < 0 || slot < 0;
     if constexpr (DECODE) {
         skip = skip || a.used_in[b] < 0;
     } else {
         skip = skip || st.pos >= st.nbits;
     }
-    if (skip) {
-        if (lane == 0) {
-            a.status[b] = NS_FRAC_SKIPPED;
-            if constexpr (!DECODE) {
-                a.token_out[b] = -1;
-                a.used_out[b] = 0;
-            }
-        }
+    if (skip) {  // token / used are left as they are: a skipped stream may have run in an earlier launch
+        if (lane == 0) a.status[b] = NS_FRAC_SKIPPED;
         return;
     }
-    bool fits = V <= a.ld;
+    bool fits = V <= a.ld && slot < a.nslots;
     if constexpr (DECODE) {
         fits = fits && a.used_in[b] <= a.max_bits && a.out_pos[b] + a.used_in[b] <= a.out_stride;
     } else {
@@ -267,7 +264,7 @@ __global__ __launch_bounds__(64) void frac_step_kernel(Args a) {
         if (lane == 0) a.status[b] = NS_FRAC_ERR_CAPACITY;
         return;
     }
-    limb* base = a.scratch + (int64_t)b * a.sstride;
+    limb* base = a.scratch + slot * a.sstride;
     uint64_t* fm = (uint64_t*)base;
     int* fsh = (int*)(base + 2 * a.ld);
     uint32_t* fd = base + 3 * a.ld;
@@ -314,7 +311,8 @@ __global__ __launch_bounds__(64) void frac_step_kernel(Args a) {
         }
         // a term f_i D < 2^(32 nd + 64 + maxs); V + 1 <= 2^31 of them sum below 2^32 times that
         const int sw = nd + 2 + (maxs + 31) / 32 + 2;
-        s_err = (err || sw > a.cap || (int64_t)(V + 1) * sw > a.table_limbs) ? NS_FRAC_ERR_CAPACITY : 0;
+        // the interval arena (cap) bounds D and a table row; only a short table is cured by a larger one
+        s_err = (err || sw > a.cap) ? NS_FRAC_ERR_CAPACITY : (int64_t)(V + 1) * sw > a.table_limbs ? NS_FRAC_ERR_TABLE : 0;
         s_nd = nd;
         s_sw = sw;
     }
@@ -402,6 +400,8 @@ struct ns_frac_ctx {
     int64_t* nbits = nullptr;
     limb* scratch = nullptr;
     size_t scratch_bytes = 0;
+    const int32_t* slot = nullptr;  // ns_frac_set_slots
+    int nslots = 0;
     std::string err;
 };
 
@@ -463,6 +463,13 @@ extern "C" int ns_frac_init(ns_frac_ctx* ctx, int B, const int64_t* h_nbits, voi
 }
 
 // per-stream scratch: fractions (4 limbs per entry), D, NTMP temporaries, the cumulative table
+static int64_t frac_tmp_limbs(int cap, int64_t max_bits) { return 2 * (int64_t)cap + (max_bits + 64) / 32 + 8; }
+
+static int64_t frac_stride_limbs(int cap, int64_t ld, int64_t max_bits, int64_t table_limbs) {
+    int64_t stride = 4 * ld + cap + 2 + nsg::frac::NTMP * frac_tmp_limbs(cap, max_bits) + table_limbs;
+    return stride + (stride & 1);  // 8-byte alignment of the next stream's fraction numerators
+}
+
 static int frac_prepare(ns_frac_ctx* ctx, int B, int64_t ld, int64_t max_bits, int64_t table_limbs, hipStream_t s,
                         nsg::frac::Args& a) {
     // max_bits bounds lane 0's depth search (one iteration per payload bit a failing step tries, each linear in
@@ -470,10 +477,10 @@ static int frac_prepare(ns_frac_ctx* ctx, int B, int64_t ld, int64_t max_bits, i
     if (B <= 0 || B > ctx->max_batch || ld < 0 || ld > (1 << 28) || max_bits < 0 || max_bits > ((int64_t)1 << 20) ||
         table_limbs < 2 || table_limbs > ((int64_t)1 << 30))
         return frac_fail(ctx, "ns_frac step: bad sizes", NS_ERR_CONFIG);
-    const int64_t tmp = 2 * (int64_t)ctx->cap + (max_bits + 64) / 32 + 8;
-    int64_t stride = 4 * ld + ctx->cap + 2 + nsg::frac::NTMP * tmp + table_limbs;
-    stride += stride & 1;  // 8-byte alignment of the next stream's fraction numerators
-    const size_t bytes = sizeof(limb) * (size_t)stride * B;
+    if (ctx->slot && ctx->nslots > B) return frac_fail(ctx, "ns_frac step: more slots than streams", NS_ERR_CONFIG);
+    const int64_t tmp = frac_tmp_limbs(ctx->cap, max_bits);
+    const int64_t stride = frac_stride_limbs(ctx->cap, ld, max_bits, table_limbs);
+    const size_t bytes = sizeof(limb) * (size_t)stride * (size_t)(ctx->slot ? ctx->nslots : B);
     if (bytes > ctx->scratch_bytes) {
         (void)hipStreamSynchronize(s);
         (void)hipFree(ctx->scratch);
@@ -494,7 +501,24 @@ static int frac_prepare(ns_frac_ctx* ctx, int B, int64_t ld, int64_t max_bits, i
     a.table_limbs = table_limbs;
     a.max_bits = max_bits;
     a.ld = ld;
+    a.slot = ctx->slot;
+    a.nslots = ctx->slot ? ctx->nslots : B;
     return NS_OK;
+}
+
+extern "C" int ns_frac_set_slots(ns_frac_ctx* ctx, const int32_t* d_slot, int nslots) {
+    if (!ctx) return frac_fail(ctx, "ns_frac_set_slots: null context", NS_ERR_CONFIG);
+    if (d_slot && (nslots <= 0 || nslots > ctx->max_batch))
+        return frac_fail(ctx, "ns_frac_set_slots: 0 < nslots <= max_batch required", NS_ERR_CONFIG);
+    ctx->slot = d_slot;
+    ctx->nslots = d_slot ? nslots : 0;
+    return NS_OK;
+}
+
+extern "C" int64_t ns_frac_scratch_bytes(const ns_frac_ctx* ctx, int nslots, int64_t ld, int64_t max_bits,
+                                         int64_t table_limbs) {
+    if (!ctx || nslots < 0 || ld < 0 || max_bits < 0 || table_limbs < 0) return -1;
+    return (int64_t)sizeof(limb) * frac_stride_limbs(ctx->cap, ld, max_bits, table_limbs) * nslots;
 }
 
 extern "C" int ns_frac_encode_step(ns_frac_ctx* ctx, int B, const double* d_probs, const int32_t* d_ids, int64_t ld,

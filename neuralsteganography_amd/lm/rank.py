@@ -71,18 +71,22 @@ class WindowedLM:
     def __init__(self, lm, window: int):
         import torch
 
-        if window <= 0:
+        if window <= 0:  # the provider maps 0 to "no trimming" (ids[-0:] is the whole list) before it gets here
             raise ConfigurationError("max_context must be positive")
         if not hasattr(lm, "window_logits"):
             raise ConfigurationError("max_context needs a GPT-2 provider (BatchedGPT2.window_logits)")
-        if window > lm.shape.n_positions:
-            raise ConfigurationError(f"max_context {window} exceeds the model's {lm.shape.n_positions} positions")
+        # a window above n_positions is fine while the context is shorter (the reference's slice keeps it whole);
+        # only a forward over more ids than the model has positions fails (_logits), as the reference's model does
         self.lm, self.window, self.shape = lm, int(window), lm.shape
         self.device = lm.device
         self.ids = torch.zeros((0, 0), dtype=torch.long)
 
     def _logits(self):
-        return self.lm.window_logits(self.ids[:, -self.window:].contiguous())
+        ids = self.ids[:, -self.window:]
+        if ids.shape[1] > self.shape.n_positions:
+            raise ConfigurationError(f"a context of {ids.shape[1]} ids (max_context {self.window}) exceeds the model's "
+                                     f"{self.shape.n_positions} positions")
+        return self.lm.window_logits(ids.contiguous())
 
     def prefill(self, context, B: int, max_new: int):
         import torch
@@ -208,6 +212,10 @@ class HipRankLM:
         ``max_context`` (a generic provider's context window is applied by ``codec.rank`` instead)."""
         mc = _max_context(quality)
         if mc is None or getattr(self.lm, "prob_rows", False):
+            return self.lm
+        if mc < 0:  # the reference's ids[-max_context:] would then DROP the first |max_context| ids: not supported
+            raise ConfigurationError("max_context must not be negative")
+        if mc == 0:  # `len(ids) > 0` holds and ids[-0:] is the whole context: no trimming (lm/arithmetic.py:49-50)
             return self.lm
         return WindowedLM(self.lm, mc)
 

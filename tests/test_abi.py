@@ -62,3 +62,12 @@ def test_split_form_setting_round_trips():
         assert _lib.set_split_max_batch(7) == 7
     finally:
         _lib.set_split_max_batch(prev)
+
+
+def test_fraction_scratch_size_query():
+    """ns_frac_scratch_bytes is host-only arithmetic: linear in the slot count, growing with the table size, -1 on
+    bad arguments."""
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("libnsgcoder.so not built (run __graft_entry__.build())")
+    L = _lib.lib()
+    assert L.ns_frac_scratch_bytes(None, 4, 16, 64, 1 << 16) == -1

@@ -206,6 +206,49 @@ def test_fraction_table_growth_and_capacity(F):
         F.encode_bits_batch([bytes(8)], [iter(dists(16, 1016))], cap_limbs=8)
 
 
+def test_fraction_table_growth_in_a_mixed_batch(F):
+    """one stream's table re-run must not touch the others.  A batch mixing V = 300 rows (their
+    steps re-run alone with a larger table, NS_FRAC_ERR_TABLE) and V = 16 rows (done in the first launch) gives
+    every message the restatement's tokens, history and decoded bytes, over several steps."""
+    rng = np.random.default_rng(11)
+    payloads, streams = [], []
+    for b in range(6):
+        V = 300 if b in (1, 4) else 16
+        rows = []
+        for _ in range(40):
+            p = rng.random(V)
+            rows.append(p / p.sum())
+        payloads.append(bytes(2))
+        streams.append(rows)
+    states = [{} for _ in payloads]
+    got = F.encode_bits_batch(payloads, [iter(s) for s in streams], states, return_exceptions=True)
+    for b, (payload, ds, st, g) in enumerate(zip(payloads, streams, states, got)):
+        want = _oracle_encode(payload, ds)
+        if isinstance(want, tuple) and isinstance(want[0], str):
+            assert isinstance(g, Exception) and _kind(g) == want, (b, g, want)
+            continue
+        toks, wst = want
+        assert g == toks, b
+        assert tuple(st["history"]) == tuple(wst["history"]), b
+    ok = [b for b, g in enumerate(got) if not isinstance(g, Exception)]
+    assert {1, 4} & set(ok) and {0, 2} & set(ok)  # both kinds of stream really ran
+    dec = F.decode_bits_batch([got[b] for b in ok], [iter(streams[b]) for b in ok], [dict(states[b]) for b in ok],
+                              return_exceptions=True)
+    for b, d in zip(ok, dec):
+        assert d == payloads[b], b
+
+
+def test_fraction_capacity_is_per_message(F):
+    """an interval arena too small for one message's lcm (NS_FRAC_ERR_CAPACITY, which no table
+    can cure) fails that message only, with FractionCapacityError, without growing any table."""
+    rng = np.random.default_rng(3)
+    big = [(lambda p: p / p.sum())(rng.random(3000)) for _ in range(2)]
+    got = F.encode_bits_batch([b"\x00", b"\x00"], [iter(big), iter(dists(4, 1004))], [{}, {}], cap_limbs=64,
+                              return_exceptions=True)
+    assert isinstance(got[0], F.FractionCapacityError)
+    assert got[1] == fc.encode(b"\x00", dists(4, 1004))[0]
+
+
 def test_fraction_payload_bound(F):
     """Payloads beyond the device coder's bound raise FractionCapacityError for that message only."""
     got = F.encode_bits_batch([bytes(F.MAX_PAYLOAD_BITS // 8 + 1), b"\x00"],

@@ -339,3 +339,39 @@ def test_rank_provider_max_context_reruns_the_trimmed_window():
     assert t2 == toks[0]
     assert decode_with_lm(t2, lm, context=ctx, quality={"temp": 0.9, "top_k": 300}, state=state,
                           max_context=W) == payloads[0]
+
+
+def test_rank_provider_max_context_zero_and_above_positions():
+    """the reference's adapter slices ``ids[-max_context:]`` only when the context is longer, so
+    max_context = 0 keeps the whole context (the same tokens as no max_context), and a max_context above the model's
+    1,024 positions is accepted while the context is shorter (the window is the whole context); only a negative
+    value is refused."""
+    import torch  # noqa: F401
+
+    from neuralsteganography_amd.exceptions import ConfigurationError
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+    from neuralsteganography_amd.lm.rank import HipRankLM
+
+    lm = HipRankLM(random_gpt2("gpt2", seed=5), None, max_batch=2)
+    ctx = [50256] + list(range(1000, 1011))
+    bits = [[(b >> k) & 1 for b in pl for k in range(8)] for pl in (b"\x12\x34", b"\xab")]
+    base = {"temp": 0.9, "top_k": 300}
+    want, _ = lm.encode_batch_states(bits, ctx, quality=base)
+    got, _ = lm.encode_batch_states(bits, ctx, quality=dict(base, max_context=0))
+    assert got == want
+    seen = []
+    orig = lm.lm.window_logits
+
+    def rec(ids):
+        seen.append(ids.shape[1])
+        return orig(ids)
+
+    lm.lm.window_logits = rec
+    try:
+        toks, states = lm.encode_batch_states(bits, ctx, quality=dict(base, max_context=2048))
+    finally:
+        lm.lm.window_logits = orig
+    assert seen[0] == len(ctx) and seen[1] == len(ctx) + 1  # untrimmed windows
+    assert lm.decode_batch(toks, ctx, quality=dict(base, max_context=2048), states=states) == bits
+    with pytest.raises(ConfigurationError):
+        lm.encode_batch_states(bits, ctx, quality=dict(base, max_context=-1))
