@@ -75,10 +75,16 @@ def parse(argv=None):
     ap.add_argument("--optin-window", type=int, default=256,
                     help="side line with the opt-in modes: fp8 KV cache + this attention window (0: skip)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-logits (PCIe-inclusive) side figure")
+    ap.add_argument("--no-attention-bench", action="store_true",
+                    help="skip the decode-attention roofline (roofline_attention)")
     ap.add_argument("--no-fraction", action="store_true", help="skip the src Fraction-coder side line (row a12)")
     ap.add_argument("--fraction-batch", type=int, default=1024)
     ap.add_argument("--fraction-vocab", type=int, default=16)
     ap.add_argument("--fraction-bytes", type=int, default=32)
+    ap.add_argument("--no-trained", action="store_true",
+                    help="skip the trained-entropy side line (GPT-2-small head scaled so rows carry a few bits/token)")
+    ap.add_argument("--trained-scale", type=float, default=8.0)
+    ap.add_argument("--trained-payload-bytes", type=int, default=512)
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)
@@ -282,6 +288,70 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
+def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3):
+    """The decode attention of the headline's step alone (``ns_decode_attention_prefix``, ``decode_attn_kernel``:
+    ~80 % of the C3 step): one GPT-2-small layer at the e2e batch, the shared 32-position context stored once and
+    each stream's own rows in chunk planes, cache length ``L`` (default: the C3 job's mean attended length), random
+    fp16 K/V/q.  K launches timed with HIP events on the launch stream.  Algorithmic bytes per launch (DESIGN
+    §4b): B·H·(L+1−T0)·2·D·2 (each stream's K and V rows, the new one included) + H·T0·2·D·2 (the shared prefix)
+    + B·3C·2 (qkv) + B·C·2 (out).  Returns the ``roofline_attention`` object."""
+    import math
+
+    import torch
+
+    from neuralsteganography_amd import _lib
+    from neuralsteganography_amd.coder import _stream_handle
+
+    B, H, D, T0 = args.e2e_batch, 12, 64, 32
+    C = H * D
+    L = int(L or 544)
+    rows = L + 1 - T0
+    nch = (rows + 31) // 32
+    g = torch.Generator(device=dev)
+    g.manual_seed(77 + rank)
+    kc = torch.randn((nch, B, H, 32, D), generator=g, device=dev, dtype=torch.float16)
+    vc = torch.randn((nch, B, H, 32, D), generator=g, device=dev, dtype=torch.float16)
+    kp = torch.randn((H, T0, D), generator=g, device=dev, dtype=torch.float16)
+    vp = torch.randn((H, T0, D), generator=g, device=dev, dtype=torch.float16)
+    qkv = torch.randn((B, 3 * C), generator=g, device=dev, dtype=torch.float16)
+    out = torch.empty((B, C), device=dev, dtype=torch.float16)
+    lib = _lib.lib()
+    st = _stream_handle()
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        rc = lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(1),
+                                            kc.stride(2), kc.stride(0), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0,
+                                            B, H, D, L, None, T0 + nch * 32, 0, out.data_ptr(), out.stride(0),
+                                            1.0 / math.sqrt(D), st)
+        if rc != 0:
+            raise RuntimeError(f"ns_decode_attention_prefix failed ({rc})")
+
+    for _ in range(warmup):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = e0.elapsed_time(e1) / steps
+    if not torch.isfinite(out.float()).all():
+        raise RuntimeError("attention bench: non-finite output")
+    alg = B * H * rows * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * C * 2 + B * C * 2
+    achieved = alg / (kern_ms / 1e3) / 1e9
+    del kc, vc, kp, vp, qkv, out
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None, "kernel": "decode_attn_kernel<FmtF16,8> (ns_decode_attention_prefix)",
+            "kernel_ms_avg": kern_ms, "launches": steps, "alg_bytes_per_launch": alg,
+            "workload": f"one GPT-2-small layer, {B} streams x {H} heads, cache length L = {L} (T0 = {T0} shared "
+                        f"context positions + {rows} own rows incl. the new one, chunk planes), fp16",
+            "alg_bytes_formula": "B*H*(L+1-T0)*2*D*2 + H*T0*2*D*2 + B*3C*2 + B*C*2",
+            "timing": "K eager launches between two HIP events on the launch stream"}
+
+
 def rank_payloads(total, world, rank, nbytes):
     """This rank's payload bit lists: streams ``shard_range(total, world, rank)`` (contiguous slices), stream s
     carrying ``synthetic.payload_bytes(s, nbytes)`` as LSB-first bits, so the union over ranks is
@@ -344,7 +414,7 @@ def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=
 
 
 def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, model=None, topk=None,
-               decode=False):
+               decode=False, logit_scale=1.0, payload_bytes=None):
     """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
     compute, HIP decode step) + HIP coder step per token, every stream encoding its full payload from the shared
     32-token context until the last stream is done (lockstep, like the reference's per-message loop run for all
@@ -358,10 +428,11 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     B = batch or args.e2e_batch
     model = model or args.e2e_model
     topk = topk or args.topk
+    nbytes = payload_bytes or args.e2e_payload_bytes
     if args.blas:
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(model), None, device=str(dev), logits_dtype=args.e2e_logits,
-                         max_batch=B, kv_dtype=kv_dtype, attention_window=window)
+                         max_batch=B, kv_dtype=kv_dtype, attention_window=window, logit_scale=logit_scale)
     lm.lm.position_cap = args.e2e_kv_cap
     lm.lm.chunked_cache = args.e2e_kv_layout == "chunked"
     quality = {"temp": args.temp, "precision": args.precision, "topk": topk}
@@ -372,7 +443,7 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     # allocated and written once (a fresh process's first pass over ~250 GB of new allocations measured up to
     # 12 % slower per step than later ones), and handed back to PyTorch's caching allocator for the timed run
     lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality, graphs=graphs)
-    bits = rank_payloads(B * world, world, rank, args.e2e_payload_bytes)
+    bits = rank_payloads(B * world, world, rank, nbytes)
     lm.lm.prefill(context, B, 2 * max(len(b) for b in bits) + 64)
     lm.lm.k_cache.zero_()
     lm.lm.v_cache.zero_()
@@ -382,8 +453,9 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
     out.update({"kv_positions": lm.lm.max_len, "kv_dtype": kv_dtype, "attention_window": window or None,
                 "workload": f"{model} (random-init weights, fp16 compute, {args.e2e_logits} logits, {kv_dtype} KV "
                             f"cache, batch-invariant native decode step) + ns_encode_step (temp {args.temp}, "
-                            f"precision {args.precision}, topk {topk}), {B} streams/GPU x {args.e2e_payload_bytes}-"
+                            f"precision {args.precision}, topk {topk}), {B} streams/GPU x {nbytes}-"
                             f"byte payloads encoded to completion from a 32-token context, "
+                            + (f"head scaled x{logit_scale} (trained-entropy rows), " if logit_scale != 1.0 else "")
                             + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")})
     del lm
     torch.cuda.empty_cache()
@@ -485,7 +557,7 @@ def measured_traffic(args, version):
     import glob
 
     best = None
-    for path in sorted(glob.glob(str(ROOT / "profiles" / "pmc_traffic_*.json"))):
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "pmc_traffic_*.json")) + glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_*.json"))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
@@ -494,6 +566,37 @@ def measured_traffic(args, version):
                 and rec.get("dtype") == args.dtype and rec.get("topk") == args.topk):
             best = (rec["traffic_bytes_per_launch"], Path(path).name)
     return best
+
+
+def _attn_traffic(args, L):
+    """Per-launch HBM bytes of the attention microbenchmark from a committed PMC record of this library build
+    (tools/pmc_traffic.py --kernel decode_attn_kernel), scaled from its cache length to ``L`` by the per-row bytes."""
+    import glob
+
+    from neuralsteganography_amd import _lib
+
+    ver = _lib.version()
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_attn*.json"))):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if rec.get("library_version") == ver and rec.get("batch") == args.e2e_batch and rec.get("L"):
+            per_row = rec["traffic_bytes_per_launch"] / rec["alg_bytes_per_launch"]
+            B, H, D, T0 = args.e2e_batch, 12, 64, 32
+            alg = B * H * (L + 1 - T0) * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * H * D * 2 + B * H * D * 2
+            return per_row * alg, f"{Path(path).name} (traffic/alg ratio {per_row:.3f} at L = {rec['L']})"
+    return None, None
+
+
+def _coder_kernel_name(dtype, topk, B):
+    """The coder_step_kernel instantiation ns_encode_step launches (launch_one in csrc/nsg_coder.hip): NSK rank
+    slots per lane from K, one wave per stream above the split form's batch limit."""
+    nsk = 2 if topk <= 128 else 5 if topk <= 320 else (8 if dtype == "f32" and topk <= 512 else 12 if dtype == "f32"
+                                                         else 8)
+    nsplit = 16 if dtype == "f32" else 8
+    form = 1 if B > 6144 // nsplit else nsplit
+    return f"coder_step_kernel<{'_Float16' if dtype == 'f16' else 'float'},false,{nsk},false,{form}>"
 
 
 def coder_bench(args, rank, world, dev, dtype=None, topk=None, pcie=True):
@@ -617,7 +720,7 @@ def coder_bench(args, rank, world, dev, dtype=None, topk=None, pcie=True):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None,
-                     "kernel": f"coder_step_kernel<{'_Float16' if args.dtype == 'f16' else 'float'},false>",
+                     "kernel": _coder_kernel_name(args.dtype, args.topk, B),
                      "alg_bytes_per_launch": alg_bytes,
                      "alg_bytes_per_stream_step": per_stream_step, "stream_steps_per_launch": B},
     }
@@ -644,7 +747,7 @@ def main():
 
     log("coder sub-benchmark")
     coder = coder_bench(args, rank, world, dev)
-    roofline = coder.pop("roofline")
+    roofline_f32 = coder.pop("roofline")
     side = {}
     roofline_f16 = None
     if not args.no_f16_coder:  # the coder the headline's end-to-end step runs: fp16 rows from the head GEMM
@@ -675,6 +778,10 @@ def main():
         if not args.no_c5_guard:  # C5 with the quality guard ON: gated covers, pass rate, reveal from text
             log("C5 guard on")
             side["c5_guard"] = c5_guard(args, rank, world, dev)
+        if not args.no_trained:  # peaked (trained-LM-like) rows: longer covers, the 1/R cutoff path at scale
+            log("trained-entropy end to end")
+            side["end_to_end_trained"] = end_to_end(args, rank, world, dev, decode=True, logit_scale=args.trained_scale,
+                                                    payload_bytes=args.trained_payload_bytes)
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             log("fp8 KV end to end")
             side["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
@@ -682,6 +789,19 @@ def main():
             log("opt-in end to end")
             side["end_to_end_optin"] = end_to_end(args, rank, world, dev, kv_dtype="fp8", window=args.optin_window)
 
+    roofline_attn = None
+    if not args.no_e2e and not args.no_attention_bench:
+        # the decode attention at the C3 job's mean attended length: T0 + (lockstep steps + 1) / 2 keys
+        L_mean = 32 + (head["lockstep_steps"] + 1) // 2 if head is not None else 544
+        log(f"decode attention at L = {L_mean}")
+        roofline_attn = attention_bench(args, rank, world, dev, L=L_mean)
+        roofline_attn["traffic"], roofline_attn["traffic_source"] = _attn_traffic(args, L_mean)
+    # the headline's roofline is the coder kernel its timed region runs (fp16 rows, topk 300); the fp32 coder's
+    # figure is a side key
+    if args.no_e2e or roofline_f16 is None or args.e2e_logits != "f16":
+        roofline, roofline_side = roofline_f32, roofline_f16
+    else:
+        roofline, roofline_side = roofline_f16, roofline_f32
     cfg = {"global_batch": args.batch * world, "vocab": args.vocab, "precision": args.precision, "topk": args.topk,
            "temp": args.temp, "parallelism": f"dp{world} (independent streams, no collective)"}
     if head is not None:
@@ -708,8 +828,10 @@ def main():
                               payload_bytes=args.payload_bytes),
                "cover_tokens_per_s": coder["cover_tokens_per_s"], "roofline": roofline, "coder": coder}
     out.update(side)
-    if roofline_f16 is not None:
-        out["roofline_f16"] = roofline_f16
+    if roofline_side is not None:
+        out["roofline_coder_f32" if roofline is roofline_f16 else "roofline_f16"] = roofline_side
+    if roofline_attn is not None:
+        out["roofline_attention"] = roofline_attn
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baselines")
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_baseline_seconds)

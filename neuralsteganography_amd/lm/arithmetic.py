@@ -157,7 +157,7 @@ class HipArithmeticLM:
 
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
                  compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096,
-                 kv_dtype: str = "fp16", attention_window: int = 0):
+                 kv_dtype: str = "fp16", attention_window: int = 0, logit_scale: float = 1.0):
         import torch
 
         from .gpt2 import BatchedGPT2
@@ -168,7 +168,8 @@ class HipArithmeticLM:
             raise NativeLibraryError("HipArithmeticLM needs a ROCm GPU (the coder has no CPU path)")
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         ldt = torch.float16 if logits_dtype == "f16" else torch.float32
-        lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt, kv_dtype=kv_dtype)
+        lm = BatchedGPT2(model, device=dev, compute_dtype=compute_dtype, logits_dtype=ldt, kv_dtype=kv_dtype,
+                         logit_scale=logit_scale)
         if attention_window:
             if not lm.native:
                 raise ConfigurationError("an attention window needs the native fp16 decode step on the GPU")

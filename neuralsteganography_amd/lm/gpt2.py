@@ -51,7 +51,8 @@ class BatchedGPT2:
     ``compute_dtype`` is the weight/activation dtype (fp16 on the GPU by default); ``logits_dtype`` is what
     the coder reads (``torch.float32`` or ``torch.float16``)."""
 
-    def __init__(self, hf_model, *, device=None, compute_dtype=None, logits_dtype=torch.float32, kv_dtype="fp16"):
+    def __init__(self, hf_model, *, device=None, compute_dtype=None, logits_dtype=torch.float32, kv_dtype="fp16",
+                 logit_scale: float = 1.0):
         cfg = hf_model.config
         self.shape = GPT2Shape(cfg.n_layer, cfg.n_head, cfg.n_embd, cfg.vocab_size, cfg.n_positions,
                                cfg.layer_norm_epsilon)
@@ -84,8 +85,10 @@ class BatchedGPT2:
         self.lnf_w = w(pre + "ln_f.weight")
         self.lnf_b = w(pre + "ln_f.bias")
         # lm_head = wte^T padded to ld columns (zeros beyond V): logits land in the coder's row layout
+        # logit_scale != 1 (synthetic "trained-entropy" rows, bench / tests only): the head alone is scaled, so a
+        # random-init model's near-uniform rows (~15 bits of entropy) peak like a trained LM's (a few bits)
         head = torch.zeros((self.shape.n_embd, self.ld), device=dev, dtype=dt)
-        head[:, : self.shape.vocab] = self.wte.t()
+        head[:, : self.shape.vocab] = self.wte.t() if logit_scale == 1.0 else (self.wte.float().t() * float(logit_scale)).to(dt)
         self.head = head
         self.B = 0
         self.L = 0

@@ -54,10 +54,10 @@ def _record_eager(lm, bit_lists, context, quality):
     return toks, seen
 
 
-def _oracle_replay(seen, s, bits, V, quality):
-    o, _ = oracle.encode_stream(lambda t: seen[t][s], bits, banned=[V - 1, 628], temp=quality["temp"],
-                                precision=quality["precision"], topk=quality["topk"])
-    return o
+def _oracle_replay(seen, s, bits, V, quality, traces=False):
+    o, tr = oracle.encode_stream(lambda t: seen[t][s], bits, banned=[V - 1, 628], temp=quality["temp"],
+                                 precision=quality["precision"], topk=quality["topk"])
+    return (o, tr) if traces else o
 
 
 def _free_cache(lm):
@@ -66,38 +66,42 @@ def _free_cache(lm):
     torch.cuda.empty_cache()
 
 
-def _b4096_roundtrip(name, label):
-    """B = 4096 streams x 1 KiB encoded on the hipGraph-replayed product loop, decoded, every payload recovered;
-    three streams re-run alone (eager, logits captured) must give the same tokens, which the oracle replays."""
+def _b4096_roundtrip(name, label, *, B=4096, nbytes=1024, quality=Q_C3, logit_scale=1.0, sample=None):
+    """B streams (default 4096) x nbytes encoded on the hipGraph-replayed product loop, decoded, every payload
+    recovered; three streams re-run alone (eager, logits captured) must give the same tokens, which the oracle
+    replays.  Returns (tokens, the oracle's per-step traces of the sampled streams)."""
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
-    B, nbytes = 4096, 1024
     m = random_gpt2(name, seed=1234)
-    lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=B)
+    lm = HipArithmeticLM(m, None, logits_dtype="f16", max_batch=B, logit_scale=logit_scale)
     # [<|endoftext|>] + 31 ids (SURVEY §8(d)); the end-of-text id is the vocabulary's last (gpt2-fa: 42,000)
     ctx = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in range(B)]
     t0 = time.perf_counter()
-    toks = lm.encode_batch(bits, ctx, quality=Q_C3)
+    toks = lm.encode_batch(bits, ctx, quality=quality)
     t1 = time.perf_counter()
     print(f"{label} encode done: {t1 - t0:.1f} s", flush=True)
     _free_cache(lm)
-    out = lm.decode_batch(toks, ctx, quality=Q_C3)
+    out = lm.decode_batch(toks, ctx, quality=quality)
     t2 = time.perf_counter()
     bad = [s for s in range(B) if out[s][: len(bits[s])] != bits[s]]
     assert not bad, f"{label}: {len(bad)} of {B} streams did not round-trip (first: {bad[:8]})"
     ntok = sum(map(len, toks))
-    print(f"{label} round trip: V={lm.vocab}, {B} x {nbytes} B, {ntok} tokens, encode {t1 - t0:.1f} s, "
-          f"decode {t2 - t1:.1f} s", flush=True)
+    print(f"{label} round trip: V={lm.vocab}, {B} x {nbytes} B, {ntok} tokens ({8 * nbytes * B / ntok:.2f} bits/token), "
+          f"encode {t1 - t0:.1f} s, decode {t2 - t1:.1f} s", flush=True)
     _free_cache(lm)
     # oracle replay: a sample of streams alone, eager, logits captured (batch-invariant step => same logits)
-    sample = [0, 1777, B - 1]
-    sub, seen = _record_eager(lm, [bits[s] for s in sample], ctx, Q_C3)
+    sample = sample or [0, B // 2 - 271, B - 1]
+    sub, seen = _record_eager(lm, [bits[s] for s in sample], ctx, quality)
+    traces = []
     for j, s in enumerate(sample):
         assert sub[j] == toks[s], f"{label} stream {s}: alone (eager) != inside the B={B} graph-replayed batch"
-        assert _oracle_replay(seen, j, bits[s], lm.vocab, Q_C3) == toks[s], f"{label} stream {s}: HIP coder != oracle"
+        o, tr = _oracle_replay(seen, j, bits[s], lm.vocab, quality, traces=True)
+        assert o == toks[s], f"{label} stream {s}: HIP coder != oracle"
+        traces.append(tr)
     _free_cache(lm)
+    return toks, traces
 
 
 @pytest.mark.timeout(900)
@@ -111,6 +115,27 @@ def test_c4_gpt2_fa_b4096_share_1kib_roundtrip_bit_exact():
     (GPT-2-small layers, V = 42,001, end-of-text 42,000 banned with 628; random-init weights, no checkpoint
     offline) -- encode -> decode with every payload recovered, and the oracle replay (VERDICT r3 #2)."""
     _b4096_roundtrip("gpt2-fa", "C4")
+
+
+@pytest.mark.timeout(900)
+def test_c5_gpt2_medium_topk100_b1024_1kib_roundtrip_bit_exact():
+    """C5's coder parameters (VERDICT r4 #9): GPT-2-medium (random-init, fp16), topk 100, temp 0.9, precision 26,
+    one GPU's 1,024-stream share of C5's 8,192, 1 KiB payloads -- encode -> decode with every payload recovered and a
+    3-stream oracle replay (quality guard off: the guard-on path is the next test)."""
+    _b4096_roundtrip("gpt2-medium", "C5", B=1024, quality={"temp": 0.9, "precision": 26, "topk": 100})
+
+
+@pytest.mark.timeout(900)
+def test_trained_entropy_rows_b4096_roundtrip_and_cutoff_path():
+    """VERDICT r4 #8: random-init GPT-2 rows are near-uniform (~8.1 bits/token, k = topk every step).  With the head
+    scaled (logit_scale 8) the rows peak like a trained LM's (a few bits per token), so covers are longer, the KV
+    cache grows past n_positions' wrap region less evenly, and the 1/R cutoff (code_base/arithmetic.py:140-165)
+    binds on some steps (k < topk in the oracle's traces).  4,096 streams x 512 B round trip + 3-stream replay."""
+    toks, traces = _b4096_roundtrip("gpt2", "trained-entropy", nbytes=512, logit_scale=8.0)
+    bpt = 8 * 512 * len(toks) / sum(map(len, toks))
+    assert 2.5 < bpt < 6.0, bpt
+    ks = [t.k for tr in traces for t in tr]
+    assert min(ks) < Q_C3["topk"], "the 1/R cutoff never bound"
 
 
 @pytest.mark.timeout(600)

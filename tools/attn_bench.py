@@ -1,0 +1,28 @@
+"""The decode-attention microbenchmark of bench.py (roofline_attention) alone, for rocprofv3 passes.
+usage: python tools/attn_bench.py [--batch 4096] [--L 544] [--steps 20]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--L", type=int, default=544)
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+
+    import bench
+
+    args = argparse.Namespace(e2e_batch=a.batch)
+    dev = torch.device("cuda", 0)
+    rec = bench.attention_bench(args, 0, 1, dev, L=a.L, steps=a.steps)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

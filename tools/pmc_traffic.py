@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--topk", type=int, default=300)
     ap.add_argument("--kernel", default="coder_step_kernel", help="kernel name substring")
+    ap.add_argument("--L", type=int, default=None, help="attention: cache length of the run")
+    ap.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per launch of the run")
     a = ap.parse_args()
     f = kernel_values(a.fetch_csv, a.kernel)
     w = kernel_values(a.write_csv, a.kernel)
@@ -38,6 +40,11 @@ def main():
            "read_bytes_corrected": 2.0 * fetch_kb * 1024.0, "write_bytes": write_kb * 1024.0,
            "traffic_bytes_per_launch": 2.0 * fetch_kb * 1024.0 + write_kb * 1024.0,
            "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024"}
+    if a.L is not None:
+        rec["L"] = a.L
+    if a.alg_bytes is not None:
+        rec["alg_bytes_per_launch"] = a.alg_bytes
+        rec["traffic_over_alg"] = rec["traffic_bytes_per_launch"] / a.alg_bytes
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps(rec))
 
