@@ -294,6 +294,12 @@ PROVIDER_CONFIGS = {
                                               quality={"top_k": 2000, "top_p": 0.95}, nbytes=[20, 7]),
     "z6_neartie_v50257_minp_k30000": dict(provider="neartie", vocab=50257, scale=0.79,
                                           quality={"min_prob": 1.3e-5, "top_k": 30000}, nbytes=[20]),
+    # round 5: the z4 / z6 qualities over 100+ tokens per stream (more top_p / min_prob boundary
+    # crossings on the near-tie rows)
+    "z7_neartie_v50257_p09_minp_long": dict(provider="neartie", vocab=50257, scale=0.79,
+                                            quality={"top_p": 0.9, "min_prob": 2e-6}, nbytes=[190, 170]),
+    "z8_neartie_v50257_minp_k30000_long": dict(provider="neartie", vocab=50257, scale=0.79,
+                                               quality={"min_prob": 1.3e-5, "top_k": 30000}, nbytes=[180]),
 }
 
 # crypto.encode_arithmetic / decode_arithmetic over GENERIC providers (the _QualityControlledLM normalises the
@@ -303,6 +309,9 @@ CRYPTO_PROVIDER_CONFIGS = {
                                   nbytes=[24, 6]),
     "x2_neartiedict_v200000_t08_k500": dict(provider="neartiedict", vocab=200000,
                                             quality={"temperature": 0.8, "top_k": 500}, nbytes=[18]),
+    # round 5: x1's crypto quality over 100+ tokens per stream
+    "x3_neartie_v50257_p09_long": dict(provider="neartie", vocab=50257, scale=0.79, quality={"top_p": 0.9},
+                                       nbytes=[200, 160]),
 }
 
 
