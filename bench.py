@@ -83,8 +83,8 @@ def parse(argv=None):
     ap.add_argument("--fraction-bytes", type=int, default=32)
     ap.add_argument("--no-trained", action="store_true",
                     help="skip the trained-entropy side line (GPT-2-small head scaled so rows carry a few bits/token)")
-    ap.add_argument("--trained-scale", type=float, default=8.0)
-    ap.add_argument("--trained-payload-bytes", type=int, default=512)
+    ap.add_argument("--trained-scale", type=float, default=6.0, help="head scale (6: ~4.2 bits/token)")
+    ap.add_argument("--trained-payload-bytes", type=int, default=384)
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)

@@ -46,7 +46,8 @@
 #define NSG_ASM_APPEND 0
 #endif
 #ifndef NSG_F16_NATIVE
-#define NSG_F16_NATIVE 0  // 1: fp16 groups kept packed (fma_mix exponents, fp16 compares, set-bit appends; A/B)
+#define NSG_F16_NATIVE 0  // 1: fp16 groups kept packed (fma_mix exponents, packed 16-bit integer pass tests, set-bit
+                          // appends; round 5), 0: converted to fp32 first (A/B)
 #endif
 #ifndef NSG_SETBIT_APPEND
 #define NSG_SETBIT_APPEND 2  // per-lane pass masks + a set-bit loop per tile: 0 never, 1 always, 2 fp16 rows only
@@ -234,7 +235,9 @@ struct Cand {
     int cnt;
     int conv;
     int ncompact;
-    float thr;  // element passes iff x > thr
+    float thr;       // element passes iff x > thr
+    int nan;         // per lane: a NaN was appended by the packed fp16 test (the step then re-streams exactly)
+    uint32_t tbits;  // wave-uniform: bits of the largest half <= thr (-0 taken as +0), for the packed fp16 test
 };
 
 __device__ __forceinline__ uint64_t raw_entry(float x, uint32_t j) {
@@ -258,6 +261,26 @@ __device__ __forceinline__ float thr_below(float v) {
     return t < v ? t : -1.17549435e-38f;
 }
 
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2v as_h2(uint32_t w) { return __builtin_bit_cast(h2v, w); }
+__device__ __forceinline__ _Float16 half_below(float t) {  // the largest half <= t (t not NaN)
+    _Float16 h = (_Float16)t;
+    if ((float)h > t) {
+        uint16_t u = __builtin_bit_cast(uint16_t, h);
+        if (u == 0x0000u) u = 0x8001u;         // +0 -> -smallest denormal
+        else if (u & 0x8000u) u = (uint16_t)(u + 1u);  // negative: one ulp further from zero
+        else u = (uint16_t)(u - 1u);           // positive (incl. +inf -> max finite): one ulp toward zero
+        h = __builtin_bit_cast(_Float16, u);
+    }
+    return h;
+}
+// c.thr and the packed fp16 test's threshold bits together (x > thr <=> x > the largest half <= thr, for halves;
+// x > -0 <=> x > +0)
+__device__ __forceinline__ void set_thr(Cand& c, float t) {
+    c.thr = t;
+    const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, half_below(t));
+    c.tbits = __builtin_amdgcn_readfirstlane(tb == 0x8000u ? 0u : tb);
+}
 template <int W>
 __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int K, int lane) {
     float mx = x[0];
@@ -278,7 +301,7 @@ __device__ __forceinline__ void offer(Cand& c, const float (&x)[W], int j0, int 
         c.cnt = c.conv = K;
         // admit ties at the K-th value: the sample tiles are offered before the stream, so a later element can
         // carry a smaller id than the K-th key (a superset is always safe; the final selection is exact)
-        c.thr = thr_below(key_val(kappa));
+        set_thr(c, thr_below(key_val(kappa)));
         npt = 0;
 #pragma unroll
         for (int q = 0; q < W; ++q) {
@@ -410,42 +433,44 @@ __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], con
 // v_fma_mix), the candidate test as an fp16 compare against the largest half <= thr (x > thr <=> x > that half
 // for every half x), and the passing values picked by a set-bit loop and converted one by one -- instead of
 // converting all 32 values of a group to fp32 first.
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ h2v as_h2(uint32_t w) { return __builtin_bit_cast(h2v, w); }
-__device__ __forceinline__ _Float16 half_below(float t) {  // the largest half <= t (t not NaN)
-    _Float16 h = (_Float16)t;
-    if ((float)h > t) {
-        uint16_t u = __builtin_bit_cast(uint16_t, h);
-        if (u == 0x0000u) u = 0x8001u;         // +0 -> -smallest denormal
-        else if (u & 0x8000u) u = (uint16_t)(u + 1u);  // negative: one ulp further from zero
-        else u = (uint16_t)(u - 1u);           // positive (incl. +inf -> max finite): one ulp toward zero
-        h = __builtin_bit_cast(_Float16, u);
-    }
-    return h;
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sub_sat16x2(uint32_t a, uint32_t b) {  // v_pk_sub_i16 ... clamp
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, a),
+                                                                      __builtin_bit_cast(s16x2, b)));
+}
+// Pass bits of one fp16 tile (8 halves of a lane, q = 2 * word + half) against t16 = the largest half <= thr, two
+// halves per instruction, as 16-bit integers.  For t16 >= +0: x > t16 <=> int16(x) > int16(t16) (negative halves are
+// negative integers, never above).  For t16 < 0: x > t16 <=> uint16(x) < uint16(t16) (x <= t means x negative with
+// bits >= t's) <=> int16(x ^ 0x7FFF) > int16(t16 ^ 0x7FFF) (flip the sign bit to compare as int16, then complement
+// to turn < into >).  So with XM = 0 or 0x7FFF per half: pass <=> sat(TT - (x ^ XM)) < 0, TT = t16 ^ XM -- the sign
+// of one clamped v_pk_sub_i16 per two halves; v_perm gathers the eight sign bytes: bits 7, 15, 23, 31 are q = 0..3,
+// bits 6, 14, 22, 30 are q = 4..7.  Exact for every half but positive NaNs, which pass here and are caught when
+// appended (Cand::nan).
+__device__ __forceinline__ uint32_t pass_bits_h(const uint4& v, uint32_t XM2, uint32_t TT2) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t sg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sg[i] = sub_sat16x2(TT2, w[i] ^ XM2);
+    const uint32_t D = __builtin_amdgcn_perm(sg[1], sg[0], 0x07050301u);
+    const uint32_t E = __builtin_amdgcn_perm(sg[3], sg[2], 0x07050301u);
+    return (D & 0x80808080u) | ((E >> 1) & 0x40404040u);
 }
 template <int G>
 __device__ __forceinline__ void offer_group_h(Cand& c, const uint4 (&raw)[G], const int (&tb)[G], int lj, int K,
                                               int lane) {
-    const _Float16 t16 = half_below(c.thr);
+    const uint32_t XM2 = (c.tbits & 0x8000u) ? 0x7FFF7FFFu : 0u;  // wave-uniform (set_thr)
+    const uint32_t TT2 = (c.tbits * 0x10001u) ^ XM2;
     uint32_t pm[G];
     int n = 0;
 #pragma unroll
     for (int d = 0; d < G; ++d) {
-        const uint32_t wd[4] = {raw[d].x, raw[d].y, raw[d].z, raw[d].w};
-        uint32_t m = 0u;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const h2v h = as_h2(wd[w]);
-            m |= (h.x > t16 ? 1u : 0u) << (2 * w);
-            m |= (h.y > t16 ? 1u : 0u) << (2 * w + 1);
-        }
-        pm[d] = m;
-        n += __builtin_popcount(m);
+        pm[d] = pass_bits_h(raw[d], XM2, TT2);
+        n += __builtin_popcount(pm[d]);
     }
     int excl, total;
     wave_excl_prefix(n, excl, total);
     if (total == 0) return;
-    if (c.cnt + total > CAND) {  // the per-tile path (compacts as needed) on fp32 values
+    if (c.cnt + total > CAND) {  // the per-tile path (compacts as needed) on fp32 values (NaN never passes there)
 #pragma unroll
         for (int d = 0; d < G; ++d) {
             float x[8];
@@ -460,10 +485,12 @@ __device__ __forceinline__ void offer_group_h(Cand& c, const uint4 (&raw)[G], co
         uint32_t m = pm[d];
         while (ballot(m != 0u)) {
             if (m) {
-                const uint32_t q = (uint32_t)__builtin_ctz(m);
+                const uint32_t bp = (uint32_t)__builtin_ctz(m);
                 m &= m - 1u;
+                const uint32_t q = (bp >> 3) + ((bp & 1u) ? 0u : 4u);
                 const uint32_t wsel = (q & 4u) ? ((q & 2u) ? raw[d].w : raw[d].z) : ((q & 2u) ? raw[d].y : raw[d].x);
                 const float v = Elem<_Float16>::h2f((q & 1u) ? (wsel >> 16) : (wsel & 0xFFFFu));
+                c.nan |= (v != v) ? 1 : 0;
                 c.keys[pos] = raw_entry(v, (uint32_t)(tb[d] + lj) + q);
                 ++pos;
             }
@@ -684,7 +711,7 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     __shared__ uint64_t s_keys[NWG][CAND];
     __shared__ __attribute__((aligned(16))) uint32_t s_scr[NWG][SCR_U32];
     __shared__ double s_part[NSPLIT > 1 ? NSPLIT : 1][3];  // split: per-wave fast-sum partials
-    __shared__ int s_cnt[NSPLIT > 1 ? NSPLIT : 1][3];      // split: cnt, conv, ncompact
+    __shared__ int s_cnt[NSPLIT > 1 ? NSPLIT : 1][4];      // split: cnt, conv, ncompact, NaN appended
 
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -720,7 +747,8 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     cand.cnt = 0;
     cand.conv = 0;
     cand.ncompact = 0;
-    cand.thr = -__builtin_inff();
+    set_thr(cand, -__builtin_inff());
+    cand.nan = 0;
     int nfallback = 0;
 
     // ---------------- stream order ----------------
@@ -816,7 +844,7 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
             if (n >= p.spec_j) pre = c;
         }
         if (pre > 0x00800000u) {
-            cand.thr = unord32(pre - 1u);
+            set_thr(cand, unord32(pre - 1u));
             spec = true;
         }
     } else if (spec_on) {
@@ -854,11 +882,11 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
             if (n >= p.spec_j) pre = c;
         }
         if (pre > 0x00800000u) {  // above ord(-inf): a finite threshold
-            cand.thr = unord32(pre - 1u);  // x > thr  <=>  ord(x) >= pre
+            set_thr(cand, unord32(pre - 1u));  // x > thr  <=>  ord(x) >= pre
             spec = true;
         }
     }
-    if (p.flags & NS_STEP_DIAG_NO_CANDIDATES) cand.thr = __builtin_inff();
+    if (p.flags & NS_STEP_DIAG_NO_CANDIDATES) set_thr(cand, __builtin_inff());
 
     NSG_STAMP(p, b, lane, 1);
     // ---------------- streaming pass (the HBM-bound part) ----------------
@@ -972,19 +1000,21 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
                 buf[d] = rd.vec(tid[d] * WAVE + lane);
             }
             if (!(jt[PREFETCH - 1] == ntiles - 1 || next_ban < (jt[PREFETCH - 1] + 1) * TS)) {
-                // the usual group: no masked id, values stay packed
-                float a = 0.0f, a1 = 0.0f;
+                // the usual group: no masked id, values stay packed (v_fma_mix exponents, two fp32 chains in
+                // v_pk_add_f32: 16 terms each, within the (PREFETCH * W + 1) u bound of the tail)
+                f32x2 a2 = {0.0f, 0.0f};
 #pragma unroll
                 for (int d = 0; d < PREFETCH; ++d) {
                     const uint32_t wd[4] = {raw[d].x, raw[d].y, raw[d].z, raw[d].w};
 #pragma unroll
                     for (int w = 0; w < 4; ++w) {
                         const h2v h = as_h2(wd[w]);
-                        a += __builtin_amdgcn_exp2f(__builtin_fmaf((float)h.x, c32, nrc));
-                        a1 += __builtin_amdgcn_exp2f(__builtin_fmaf((float)h.y, c32, nrc));
+                        const f32x2 e2 = {__builtin_amdgcn_exp2f(__builtin_fmaf((float)h.x, c32, nrc)),
+                                          __builtin_amdgcn_exp2f(__builtin_fmaf((float)h.y, c32, nrc))};
+                        a2 += e2;
                     }
                 }
-                acc64 += (double)(a + a1);
+                acc64 += (double)(a2.x + a2.y);
                 offer_group_h<PREFETCH>(cand, raw, tb, lane * W, K, lane);
                 continue;
             }
@@ -1041,6 +1071,8 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
             s_cnt[wv][1] = cand.conv;
             s_cnt[wv][2] = cand.ncompact;
         }
+        const bool wave_nan = ballot(cand.nan != 0) != 0ull;
+        if (lane == 0) s_cnt[wv][3] = wave_nan ? 1 : 0;
         __syncthreads();
         if (wv != 0) return;
         double ta = 0.0, tb = 0.0, tu = 0.0;
@@ -1056,6 +1088,7 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
         for (int v = 1; v < NSPLIT; ++v) {
             const int n = s_cnt[v][0], cv = s_cnt[v][1];
             cand.ncompact += s_cnt[v][2];
+            cand.nan |= s_cnt[v][3];
             const uint64_t* src = s_keys[v];
             for (int i0 = 0; i0 < n; i0 += WAVE) {
                 if (cand.cnt + WAVE > CAND) {  // cnt > CAND - 64 >= K
@@ -1076,11 +1109,14 @@ __global__ __launch_bounds__((NSPLIT > 1 ? NSPLIT : WPB) * WAVE, NSG_MIN_WAVES_P
     }
     // speculation check: the buffer holds the true top-K iff at least K elements passed the guess
     // (or a compaction happened, which needs > CAND - TS >= K passes).  Else re-stream, exactly.
-    if (spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) {
+    // (a positive NaN appended by the packed fp16 test also re-streams: the fp32 test below never admits NaN)
+    const bool nan_cand = ballot(cand.nan != 0) != 0ull;
+    if ((spec && cand.ncompact == 0 && cand.cnt < K && !(p.flags & NS_STEP_DIAG_NO_CANDIDATES)) || nan_cand) {
         ++nfallback;
         cand.cnt = 0;
         cand.conv = 0;
-        cand.thr = -__builtin_inff();
+        cand.nan = 0;
+        set_thr(cand, -__builtin_inff());
         int bj = 0, nbj = p.nbanned > 0 ? p.banned[0] : 0x7FFFFFFF;
         for (int tile = 0; tile < ntiles; ++tile) {
             float x[W];

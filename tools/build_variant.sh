@@ -1,12 +1,20 @@
 #!/bin/bash
 # Compile a tuning variant of the coder library: tools/build_variant.sh NAME [-DMACRO=VALUE ...]
-# -> neuralsteganography_amd/_build/variants/NAME.so (same sources as __graft_entry__.build()).
+# -> neuralsteganography_amd/_build/variants/NAME.so (same sources as __graft_entry__.build(), one object per source
+# compiled in parallel).
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
-mkdir -p "$root/neuralsteganography_amd/_build/variants"
+out=$root/neuralsteganography_amd/_build/variants
+mkdir -p "$out/obj_$name"
 c=$root/neuralsteganography_amd/csrc
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wno-unused-function \
-    -I "$root/include" "$@" -o "$root/neuralsteganography_amd/_build/variants/$name.so" \
-    "$c/nsg_coder.hip" "$c/nsg_wide.hip" "$c/nsg_attn.hip" "$c/nsg_score.hip" "$c/nsg_lm.hip" "$c/nsg_fraction.hip"
+pids=()
+for s in nsg_coder nsg_wide nsg_attn nsg_score nsg_lm nsg_fraction; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function \
+      -I "$root/include" "$@" -c -o "$out/obj_$name/$s.o" "$c/$s.hip" 2>/dev/null &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/$name.so" "$out"/obj_$name/*.o
+rm -rf "$out/obj_$name"
 echo "built variants/$name.so $*"
