@@ -52,6 +52,9 @@
 #ifndef NSG_SETBIT_APPEND
 #define NSG_SETBIT_APPEND 2  // per-lane pass masks + a set-bit loop per tile: 0 never, 1 always, 2 fp16 rows only
 #endif
+#ifndef NSG_SLOT_APPEND
+#define NSG_SLOT_APPEND 0  // per-slot ballot appends (offer_slots; A/B, round 5: f16 equal, f32 +2 %): 0 off, 1 all, 2 fp16
+#endif
 #ifndef NSG_DIAG_NOWRITE
 #define NSG_DIAG_NOWRITE 0
 #endif
@@ -330,6 +333,49 @@ __device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
     }
 }
 
+// Per-slot appends of one tile (round 5): one v_cmp per value slot gives the slot's wave mask in SGPRs; the
+// capacity check and the running base are scalar; only the slots that some lane passes (a scalar branch) compute
+// a position (two mbcnt) and write, under exec = the slot's mask.  Every (tile, slot) in a 64-lane wave has a pass
+// with probability ~1 - (1 - rate)^64, so a per-lane set-bit loop runs about once per tile whatever the rate; the
+// slots cost ~4 VALU each only where they write (profiles/r05: appends were +30 us of the 121 us fp16 launch).
+template <int W>
+__device__ __forceinline__ void offer_slots(Cand& c, const float (&x)[W], int jl, int K, int lane) {
+    uint64_t msk[W];
+    int npt = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        msk[q] = ballot(x[q] > c.thr);
+        npt += popc64(msk[q]);
+    }
+    if (npt == 0) return;
+    if (c.cnt + npt > CAND) {  // the per-tile path compacts first (recomputing the tests at the raised threshold)
+        offer<W>(c, x, jl, K, lane);
+        return;
+    }
+    const uint32_t kb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t*)c.keys;
+    int base = c.cnt;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        if (msk[q] != 0ull) {  // wave-uniform
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk[q] >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)msk[q], (uint32_t)base));
+            const uint64_t e = raw_entry(x[q], (uint32_t)(jl + q));
+            uint64_t saved;
+            // exec = the slot's passing lanes for the one write (LDS ops of a wave complete in order, so the
+            // compiler's own lgkmcnt waits stay valid with this extra write in flight)
+            asm volatile(
+                "s_and_saveexec_b64 %0, %1\n\t"
+                "ds_write_b64 %2, %3\n\t"
+                "s_mov_b64 exec, %0"
+                : "=&s"(saved)
+                : "s"(msk[q]), "v"(kb + 8u * pos), "v"(e)
+                : "memory");
+            base += popc64(msk[q]);
+        }
+    }
+    c.cnt = base;
+}
+
 // Group form of offer(): G tiles (G*W values per lane) share one reject test, one wave prefix and one
 // capacity check; passing values are written with predicated stores at lane-private positions.  If the
 // group does not fit, the per-tile path (which compacts as needed and always fits) takes over.  Tile d's
@@ -338,6 +384,11 @@ __device__ __forceinline__ void wave_excl_prefix(int n, int& excl, int& total) {
 template <int W, int G>
 __device__ __forceinline__ void offer_group(Cand& c, const float (&x)[G][W], const int (&tb)[G], int lj, int K,
                                             int lane) {
+    if constexpr (NSG_SLOT_APPEND == 1 || (NSG_SLOT_APPEND == 2 && W == 8)) {
+#pragma unroll
+        for (int d = 0; d < G; ++d) offer_slots<W>(c, x[d], tb[d] + lj, K, lane);
+        return;
+    }
     // set-bit appends: measured 1.6-2.2 % faster on fp16 rows, 2 % slower on fp32 rows (profiles/r04/coder_append_ab.jsonl)
     constexpr bool SETBIT = NSG_SETBIT_APPEND == 1 || (NSG_SETBIT_APPEND == 2 && W == 8);
     int n = 0;
