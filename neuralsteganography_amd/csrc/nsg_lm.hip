@@ -833,6 +833,149 @@ __global__ __launch_bounds__(512) void gemm_pp(const f16* __restrict__ X, int64_
     }
 }
 
+// ------------------------------------------------------------------------------------------------ chains
+// gemm_chains<SK, EPI> (round 5): the SK = k_chains(K) = 2 or 4 K chains of the canonical order computed side by
+// side instead of one after the other.  A workgroup of 4 * SK waves owns one 64 x 64 tile; wave group c (4 waves of
+// 32 x 32, laid out as in gemm_tiled<64, 64, 2, 2>) runs chain c -- K-tiles [c * TPC, min((c + 1) * TPC, KT)) --
+// through its own two-stage LDS ring, and the chains meet in LDS, where group 0 adds them in order,
+// ((c0 + c1) + c2) + c3, and stores.  The same MFMA chains and the same additions as gemm_tiled's sequential SPLIT
+// form, so the bits are the same; what changes is how many waves a long-K GEMM with few output tiles keeps busy
+// (GPT-2-medium's mlp c_proj at B = 1,024: 256 tiles, one 4-wave workgroup per CU in the sequential form).
+template <int SK, int EPI>
+__global__ __launch_bounds__(256 * SK) void gemm_chains(const f16* __restrict__ X, int64_t ldx,
+                                                         const f16* __restrict__ Wt, int64_t ldw,
+                                                         const f16* __restrict__ bias, void* Y, int64_t ldy, int M,
+                                                         int N, int K) {
+    constexpr int BN = 64, BM = 64, WM = 2, FN = 2, FM = 2;
+    constexpr int ROWS = BN + BM, GL = ROWS * 8 / 256;  // 16-byte DMA pieces per thread per K-tile (4)
+    constexpr int SB = ROWS * 128;                      // one stage: 16 KiB
+    static_assert(SK == 2 || SK == 4, "chains");
+    __shared__ __attribute__((aligned(16))) char smem[SK * 2 * SB];
+
+    const int tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    constexpr int GN = 1024 / BN;
+    const int grp = t / (GN * tiles_m), within = t - grp * (GN * tiles_m);
+    const int gn = min(GN, tiles_n - grp * GN);
+    const int tm = within / gn, tn = grp * GN + (within - tm * gn);
+    const int n0 = tn * BN, m0 = tm * BM;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c = wave >> 2, ww = wave & 3;  // chain, wave within the chain group
+    const int wn = ww / WM, wm = ww - wn * WM;
+    char* ring = smem + c * 2 * SB;
+
+    const f16* src[GL];
+    int lds_off[GL];
+#pragma unroll
+    for (int g = 0; g < GL; ++g) {
+        const int q = g * 4 + ww;
+        const int row = q * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ swz(row);
+        if (row < BN)
+            src[g] = Wt + (int64_t)min(n0 + row, N - 1) * ldw + chunk * 8;
+        else
+            src[g] = X + (int64_t)min(m0 + row - BN, M - 1) * ldx + chunk * 8;
+        lds_off[g] = q * 8 * 128;
+    }
+    auto stage = [&](int kt, int buf) {
+#pragma unroll
+        for (int g = 0; g < GL; ++g)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[g] + kt * BK),
+                                             (__attribute__((address_space(3))) void*)(ring + buf * SB + lds_off[g]),
+                                             16, 0, 0);
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int KT = K / BK, TPC = (KT + SK - 1) / SK;
+    const int k0 = c * TPC, nk = max(0, min(k0 + TPC, KT) - k0);  // wave-uniform
+    const int fr = lane & 15, fc = lane >> 4;
+    if (nk > 0) stage(k0, 0);
+    int buf = 0;
+    for (int i = 0; i < TPC; ++i) {  // every chain runs TPC rounds: the workgroup barriers stay uniform
+        if (i + 1 < nk) {
+            stage(k0 + i + 1, buf ^ 1);
+            wait_vm<GL>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i < nk) {
+            const char* base = ring + buf * SB;
+            f16x8 a[2][FN], b[2][FM];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int ch = kk * 4 + fc;
+#pragma unroll
+                for (int ii = 0; ii < FN; ++ii) {
+                    const int row = wn * FN * 16 + ii * 16 + fr;
+                    a[kk][ii] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+                }
+#pragma unroll
+                for (int j = 0; j < FM; ++j) {
+                    const int row = BN + wm * FM * 16 + j * 16 + fr;
+                    b[kk][j] = *(const f16x8*)(base + row * 128 + ((ch ^ swz(row)) << 4));
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int ii = 0; ii < FN; ++ii)
+#pragma unroll
+                    for (int j = 0; j < FM; ++j) acc[ii][j] = mfma16(a[kk][ii], b[kk][j], acc[ii][j]);
+        }
+        lds_fence_barrier();  // every wave is done reading this buffer before it is refilled
+        buf ^= 1;
+    }
+    // chains 1.. hand their accumulators to group 0 through LDS (the rings are idle: every copy landed, every read
+    // completed before the last barrier); lane-fastest layout, conflict-free
+    float* red = (float*)smem;
+    if (c > 0) {
+#pragma unroll
+        for (int ii = 0; ii < FN; ++ii)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    red[((((c - 1) * 4 + ww) * 16) + (ii * FM + j) * 4 + r) * 64 + lane] = acc[ii][j][r];
+    }
+    __syncthreads();
+    if (c != 0) return;
+    f32x4 tot[FN][FM];
+#pragma unroll
+    for (int ii = 0; ii < FN; ++ii)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) tot[ii][j] = acc[ii][j];
+#pragma unroll
+    for (int cc = 1; cc < SK; ++cc) {
+#pragma unroll
+        for (int ii = 0; ii < FN; ++ii)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = red[((((cc - 1) * 4 + ww) * 16) + (ii * FM + j) * 4 + r) * 64 + lane];
+                tot[ii][j] = tot[ii][j] + v;  // ((c0 + c1) + c2) + c3, as gemm_tiled's SPLIT form
+            }
+    }
+#pragma unroll
+    for (int ii = 0; ii < FN; ++ii) {
+        const int n = n0 + wn * FN * 16 + ii * 16 + 4 * fc;
+        if (n >= N) continue;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int m = m0 + wm * FM * 16 + j * 16 + fr;
+            if (m < M) store4<EPI>(Y, ldy, bias, m, n, tot[ii][j]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ layernorm
 constexpr int LN_MAXV = 8;  // f16x4 vectors per lane: C <= 2048
 
@@ -1024,6 +1167,7 @@ enum GemmCfg {
     CFG_P128_2, CFG_P128_3, CFG_P128_4,               // persistent 128 x 128, 2 / 3 / 4 stages (2 / 1 / 1 per CU)
     CFG_PP256,                                        // 256 x 256, two ping-pong wave groups (K <= 1024)
     CFG_PP192,                                        // 192 weight rows x 256, the same ping-pong kernel
+    CFG_C64,                                          // 64 x 64, the K chains side by side (K > 1024; round 5)
     CFG_COUNT
 };
 
@@ -1123,6 +1267,18 @@ static void launch_cfg(int cfg, const f16* x, int64_t ldx, const f16* wt, int64_
                                    ldy, M, N, K);
             }
             break;
+        case CFG_C64: {
+            const int sk = k_chains(K);
+            if (sk == 4)
+                hipLaunchKernelGGL((gemm_chains<4, EPI>), tiles(64, 64), dim3(1024), 0, st, x, ldx, wt, ldw, bias, y, ldy,
+                                   M, N, K);
+            else if (sk == 2)
+                hipLaunchKernelGGL((gemm_chains<2, EPI>), tiles(64, 64), dim3(512), 0, st, x, ldx, wt, ldw, bias, y, ldy,
+                                   M, N, K);
+            else
+                NSG_TILED(64, 64, 2, 2, 2);  // one chain: the plain 64 x 64 kernel (same bits)
+            break;
+        }
         case CFG_P128_2:
         case CFG_P128_3:
         case CFG_P128_4: {
@@ -1179,6 +1335,10 @@ static int auto_cfg(int M, int N, int K) {
         return w192 < w256 ? CFG_PP192 : CFG_PP256;
     }
     if (!split && M >= 1024 && N >= 4096) return CFG_T128x64_3;
+    // long K (two or four chains) with few 64 x 64 tiles: the chains side by side (GPT-2-medium's mlp c_proj at
+    // B = 1,024: 416 vs 292 TFLOP/s sequential, hipBLASLt 365); with more tiles than two per CU the sequential
+    // form keeps more workgroups in flight (GPT-2's at B = 4,096: 540 vs 423; profiles/r05/lmprobe_r05k_*.jsonl)
+    if (split && (long)((M + 63) / 64) * ((N + 63) / 64) <= 2L * cu_count()) return CFG_C64;
     return CFG_T64_2;
 }
 
