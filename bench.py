@@ -84,7 +84,10 @@ def parse(argv=None):
     ap.add_argument("--no-trained", action="store_true",
                     help="skip the trained-entropy side line (GPT-2-small head scaled so rows carry a few bits/token)")
     ap.add_argument("--trained-scale", type=float, default=6.0, help="head scale (6: ~4.2 bits/token)")
-    ap.add_argument("--trained-payload-bytes", type=int, default=384)
+    ap.add_argument("--trained-payload-bytes", type=int, default=512)
+    ap.add_argument("--trained-batch", type=int, default=2048,
+                    help="streams of the trained-entropy leg (covers ~2x as long as C3's and uneven: the KV cache of "
+                         "4096 streams would not fit)")
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)
@@ -731,6 +734,22 @@ def coder_bench(args, rank, world, dev, dtype=None, topk=None, pcie=True):
     return out
 
 
+def _side_leg(fn):
+    """A side line's result, or {"error": ...} if it fails: on one GPU a side line never takes the headline down with
+    it (device memory is released before the next leg).  With several ranks a failure propagates: a rank that
+    skipped a leg's collectives would leave the others waiting in them."""
+    import torch
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return fn()
+    try:
+        return fn()
+    except Exception as exc:  # noqa: BLE001 - reported in the JSON line, the run goes on
+        log(f"side line failed: {type(exc).__name__}: {exc}")
+        torch.cuda.empty_cache()
+        return {"error": f"{type(exc).__name__}: {str(exc)[:300]}"}
+
+
 def main():
     args = parse()
     import torch
@@ -756,10 +775,10 @@ def main():
         roofline_f16 = side["coder_f16"].pop("roofline")
     if not args.no_wide:
         log("wide path")
-        side["wide_path"] = wide_path(args, rank, world, dev)
+        side["wide_path"] = _side_leg(lambda: wide_path(args, rank, world, dev))
     if not args.no_fraction:
         log("src Fraction coder")
-        side["fraction_coder"] = fraction_coder(args, rank, world, dev)
+        side["fraction_coder"] = _side_leg(lambda: fraction_coder(args, rank, world, dev))
     head = None
     if not args.no_e2e:
         # headline: config C3 end to end, encoded then decoded and checked
@@ -767,27 +786,29 @@ def main():
         head = end_to_end(args, rank, world, dev, decode=not args.no_decode)
         if not args.no_c2:  # C2: one message per GPU -- per-token latency of the whole step (small-batch coder form)
             log("C2 end to end")
-            side["end_to_end_c2"] = end_to_end(args, rank, world, dev, batch=1, decode=True)
+            side["end_to_end_c2"] = _side_leg(lambda: end_to_end(args, rank, world, dev, batch=1, decode=True))
         if not args.no_c4:  # C4's per-GPU share: gpt2-fa geometry (V = 42,001), 4096 streams
             log("C4 share end to end")
-            side["end_to_end_c4"] = end_to_end(args, rank, world, dev, model="gpt2-fa", decode=True)
+            side["end_to_end_c4"] = _side_leg(lambda: end_to_end(args, rank, world, dev, model="gpt2-fa", decode=True))
         if not args.no_c5:  # C5's per-GPU share: GPT-2-medium fp16, topk 100, temp 0.9, 1024 streams
             log("C5 share end to end")
-            side["end_to_end_c5"] = end_to_end(args, rank, world, dev, model="gpt2-medium", batch=1024, topk=100,
-                                               decode=True)
+            side["end_to_end_c5"] = _side_leg(lambda: end_to_end(args, rank, world, dev, model="gpt2-medium",
+                                                                 batch=1024, topk=100, decode=True))
         if not args.no_c5_guard:  # C5 with the quality guard ON: gated covers, pass rate, reveal from text
             log("C5 guard on")
-            side["c5_guard"] = c5_guard(args, rank, world, dev)
+            side["c5_guard"] = _side_leg(lambda: c5_guard(args, rank, world, dev))
         if not args.no_trained:  # peaked (trained-LM-like) rows: longer covers, the 1/R cutoff path at scale
             log("trained-entropy end to end")
-            side["end_to_end_trained"] = end_to_end(args, rank, world, dev, decode=True, logit_scale=args.trained_scale,
-                                                    payload_bytes=args.trained_payload_bytes)
+            side["end_to_end_trained"] = _side_leg(lambda: end_to_end(
+                args, rank, world, dev, decode=True, logit_scale=args.trained_scale, batch=args.trained_batch,
+                payload_bytes=args.trained_payload_bytes))
         if args.fp8kv:  # opt-in numerics mode, reported beside (never as) the fp16 reference configuration
             log("fp8 KV end to end")
-            side["end_to_end_fp8kv"] = end_to_end(args, rank, world, dev, kv_dtype="fp8")
+            side["end_to_end_fp8kv"] = _side_leg(lambda: end_to_end(args, rank, world, dev, kv_dtype="fp8"))
         if args.optin_window:  # opt-in: fp8 KV + sliding attention window (bounded per-step KV traffic)
             log("opt-in end to end")
-            side["end_to_end_optin"] = end_to_end(args, rank, world, dev, kv_dtype="fp8", window=args.optin_window)
+            side["end_to_end_optin"] = _side_leg(lambda: end_to_end(args, rank, world, dev, kv_dtype="fp8",
+                                                                    window=args.optin_window))
 
     roofline_attn = None
     if not args.no_e2e and not args.no_attention_bench:

@@ -1,8 +1,8 @@
 """Batched GPT-2 forward with a preallocated KV cache, writing logits straight into the coder's layout.
 
-This is the L1 "LM runtime" of SURVEY.md §1 rebuilt for batch B on PyTorch-ROCm (the GEMMs run on MFMA
-through rocBLAS/hipBLASLt; the coder step is the hand-written HIP kernel).  It reproduces the reference's
-forward semantics (``code_base/arithmetic.py:12-48,115-122``):
+This is the L1 "LM runtime" of SURVEY.md §1 rebuilt for batch B (PyTorch-ROCm holds the weights and the KV cache;
+in the fp16 GPU configuration every GEMM and attention of the forward runs on the library's own MFMA kernels, see
+below).  It reproduces the reference's forward semantics (``code_base/arithmetic.py:12-48,115-122``):
 
 * the first call runs the whole context with default positions ``0..T-1``;
 * every later call feeds ONE token per stream with ``position_ids = cache_len % n_positions``
