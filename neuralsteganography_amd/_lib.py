@@ -30,12 +30,13 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_encode_step", "ns_decode_step", "ns_set_sentence_end", "ns_set_stats", "ns_sample_step", "ns_set_rank_export",
            "ns_rank_encode_step", "ns_set_rank_rows", "ns_rank_decode_step", "ns_token_probs",
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
-           "ns_decode_attention_fp8", "ns_quantize_fp8",
+           "ns_decode_attention_fp8", "ns_decode_attention_ex", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
            "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm",
            "ns_frac_create", "ns_frac_destroy", "ns_frac_last_error", "ns_frac_init", "ns_frac_encode_step",
            "ns_frac_decode_step", "ns_frac_set_slots", "ns_frac_scratch_bytes")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
+NS_KV_FP16, NS_KV_FP8 = 0, 1
 
 
 class NsStreamState(ctypes.Structure):
@@ -135,6 +136,9 @@ def lib() -> ctypes.CDLL:
         f.restype = ci
         f.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, vp, i64,
                       ctypes.c_float, vp]
+    L.ns_decode_attention_ex.restype = ci
+    L.ns_decode_attention_ex.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, ci,
+                                         vp, i64, vp, i64, ctypes.c_float, vp]
     L.ns_quantize_fp8.restype = ci
     L.ns_quantize_fp8.argtypes = [vp, vp, i64, vp]
     L.ns_lm_gemm.restype = ci

@@ -154,6 +154,7 @@ class HipArithmeticLM:
     """Arithmetic-coding provider: batched GPT-2 on PyTorch-ROCm + the HIP coder step."""
 
     decodes_without_state = True  # the interval coder needs no per-token history (unlike the rank coder)
+    skip_done = True  # encode: finished streams skip their decode attention (same tokens; A/B and tests only)
 
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
                  compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096,
@@ -336,6 +337,27 @@ class HipArithmeticLM:
                 stop.flag(tok)  # device-side: did any live stream emit a token that can complete stop_text?
             return tok
 
+        native = getattr(self.lm, "native", False) and self.skip_done
+        if native:  # finished streams skip their attention reads (the coder state's flags word, NS_ST_DONE)
+            import torch
+
+            self.lm.done_flags = sess.state.view(torch.int32)[:, 7]
+        try:
+            toks = self._encode_loop(sess, coder_step, logits, stop, bit_lists, check_every, stall_steps, hard_cap,
+                                     use_graph)
+        finally:
+            if native:
+                self.lm.done_flags = None
+        for b in bit_lists:
+            st = _bits_count_state(len(b))
+            self._encode_states.append(st)
+            self._decode_states.append(dict(st))
+        if return_stats:
+            return toks, sess.stats()
+        return toks
+
+    def _encode_loop(self, sess, coder_step, logits, stop, bit_lists, check_every, stall_steps, hard_cap, use_graph):
+        B = sess.B
         t = 0
         last_pos = None
         last_move = 0
@@ -379,14 +401,7 @@ class HipArithmeticLM:
             logits = self.lm.step(tok)
             t += 1
         del graph
-        toks = sess.tokens()
-        for b in bit_lists:
-            st = _bits_count_state(len(b))
-            self._encode_states.append(st)
-            self._decode_states.append(dict(st))
-        if return_stats:
-            return toks, sess.stats()
-        return toks
+        return sess.tokens()
 
     def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], graphs: Optional[bool] = None) -> List[List[int]]:

@@ -118,11 +118,14 @@ class BatchedGPT2:
         self.kv_torch_dtype = torch.uint8 if kv_dtype == "fp8" else self.dtype
         self.d_L = None
         self._static_logits = None
+        # optional per-stream done flags read by the decode attention (int32 tensor view [B], bit 0 = finished, e.g.
+        # the coder state's flags word): finished streams skip their cache reads; their logits are never used again
+        self.done_flags = None
         if self.native:
             from .. import _lib
 
-            self._attn = (_lib.lib().ns_decode_attention_fp8 if kv_dtype == "fp8"
-                          else _lib.lib().ns_decode_attention_prefix)
+            self._attn = _lib.lib().ns_decode_attention_ex
+            self._kv_format = _lib.NS_KV_FP8 if kv_dtype == "fp8" else _lib.NS_KV_FP16
             if self.shape.n_embd // self.shape.n_head != 64:
                 raise ValueError("the HIP decode attention needs head_dim 64 (GPT-2 small/medium/large)")
             for lw in self.layers:
@@ -499,6 +502,10 @@ class BatchedGPT2:
                             st), "ns_lm_gemm")
 
         strides = [self._cache_strides(i) for i in range(s.n_layer)]
+        df = self.done_flags
+        if df is not None and (df.dtype != torch.int32 or df.shape != (B,) or df.device != self.device):
+            raise ValueError(f"done_flags must be an int32 [{B}] view on {self.device}")
+        done_ptr, done_stride = (df.data_ptr(), df.stride(0)) if df is not None else (None, 0)
         lw0 = self.layers[0]
         ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
                             self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
@@ -519,8 +526,8 @@ class BatchedGPT2:
             vp = self.vp[i, 0] if T0 else None
             rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz,
                             kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
-                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, self.window, o.data_ptr(),
-                            o.stride(0), 1.0 / math.sqrt(D), st)
+                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, self.window,
+                            self._kv_format, done_ptr, done_stride, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
             ok(rc, "ns_decode_attention_prefix")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
             ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)

@@ -612,3 +612,69 @@ def test_native_prefill_and_scoring_use_no_torch_attention_or_blas(monkeypatch):
     assert (fs[0, :, :V].double().cpu() - ref).abs().max() < 3e-2
     assert (fs[1, :, :V].double().cpu() - ref_rev).abs().max() < 3e-2
     assert (wl[0, :V].double().cpu() - ref_w).abs().max() < 3e-2
+
+
+@pytest.mark.parametrize("B,L", [(3, 40), (700, 300)])
+def test_decode_attention_done_flags_skip_finished_streams(B, L):
+    """ns_decode_attention_ex with done flags (round 5): streams whose flag bit 0 is set are skipped -- no KV
+    append, their output rows untouched -- and every other stream's output is bit-identical to the unflagged call
+    (P = 1 and P = 8 workgroup forms)."""
+    H, D, T0 = 12, 64, 8
+    C = H * D
+    g = torch.Generator(device="cuda").manual_seed(B + L)
+    cap = L + 1
+    nch = (cap - T0 + 31) // 32
+    kc = torch.randn((nch, B, H, 32, D), generator=g, device="cuda").half()
+    vc = torch.randn((nch, B, H, 32, D), generator=g, device="cuda").half()
+    kp = torch.randn((H, T0, D), generator=g, device="cuda").half()
+    vp = torch.randn((H, T0, D), generator=g, device="cuda").half()
+    qkv = torch.randn((B, 3 * C), generator=g, device="cuda").half()
+    flags = torch.zeros((B, 8), dtype=torch.int32, device="cuda")
+    flags[::3, 7] = 1  # every third stream finished
+    flags[1::3, 7] = 2  # other bits do not count
+    L_ = _lib.lib()
+
+    def run(done):
+        k2, v2 = kc.clone(), vc.clone()
+        out = torch.full((B, C), 5.0, device="cuda").half()
+        rc = L_.ns_decode_attention_ex(qkv.data_ptr(), qkv.stride(0), k2.data_ptr(), v2.data_ptr(), k2.stride(1),
+                                       k2.stride(2), k2.stride(0), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H,
+                                       D, L, None, cap, 0, _lib.NS_KV_FP16,
+                                       done.data_ptr() if done is not None else None, done.stride(0) if done is not None
+                                       else 0, out.data_ptr(), out.stride(0), 1.0 / math.sqrt(D), _stream_handle())
+        assert rc == 0
+        torch.cuda.synchronize()
+        return out, k2, v2
+
+    ref, kr, vr = run(None)
+    got, kg, vg = run(flags[:, 7])
+    live = (flags[:, 7] & 1) == 0
+    assert torch.equal(got[live], ref[live])
+    assert (got[~live] == 5.0).all()  # skipped: untouched
+    r = L - T0  # the appended row of every stream
+    assert torch.equal(kg[r // 32, live, :, r % 32], kr[r // 32, live, :, r % 32])
+    assert torch.equal(kg[r // 32, ~live, :, r % 32], kc[r // 32, ~live, :, r % 32])  # no append when skipped
+
+
+def test_encode_skip_done_streams_gives_the_same_tokens():
+    """The encode loop hands the coder state's flags to the attention (finished streams skip their cache reads):
+    ragged payloads give the same tokens with and without it, graph-replayed and eager."""
+    from neuralsteganography_amd import synthetic
+    from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
+    from neuralsteganography_amd.lm.gpt2 import random_gpt2
+
+    lm = HipArithmeticLM(random_gpt2("gpt2", seed=3), None, logits_dtype="f16", max_batch=6)
+    ctx = synthetic.DEFAULT_CONTEXT
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, n)) for s, n in enumerate((1, 40, 7, 64, 2, 30))]
+    q = {"temp": 0.9, "precision": 26, "topk": 300}
+    for graphs in (True, False):
+        lm.skip_done = True
+        a = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
+        lm.skip_done = False
+        b = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
+        assert a == b
+        assert lm.decode_batch(a, ctx, quality=q, graphs=graphs) == [o for o in lm.decode_batch(b, ctx, quality=q,
+                                                                                              graphs=graphs)]
+    lm.skip_done = True
+    out = lm.decode_batch(a, ctx, quality=q)
+    assert all(o[: len(x)] == x for o, x in zip(out, bits))
