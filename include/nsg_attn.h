@@ -75,18 +75,19 @@ int ns_decode_attention_fp8(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
 #define NS_KV_FP8 1
 
 /* ns_decode_attention_prefix (kv_format NS_KV_FP16) / ns_decode_attention_fp8 (NS_KV_FP8) with an optional
- * per-stream done flag: when d_done is not NULL, stream b is skipped if bit 0 of d_done[b * done_stride] is set
- * (uint32 words; e.g. the flags word of the coder state, NS_ST_DONE): no KV append, no cache read, its output row
- * left as it was.  The flag is read when the kernel runs, so one captured hipGraph serves every step while streams
- * finish.  The other streams' outputs are the same bits with or without the flags (a stream's row split depends
+ * per-stream end: stream b is skipped if d_done is not NULL and bit 0 of d_done[b * done_stride] is set (uint32
+ * words; e.g. the flags word of the coder state, NS_ST_DONE -- encode), or if d_stop is not NULL and the cache
+ * length L0 >= d_stop[b] (int32; the position after which a decode needs no more logits): no KV append, no cache
+ * read, its output row left as it was.  Both are read when the kernel runs (L0 from d_L0 on graph replays), so one
+ * captured hipGraph serves every step while streams finish.  The other streams' outputs are the same bits with or without the flags (a stream's row split depends
  * on its key count only): a lockstep batch whose covers differ in length (peaked, trained-LM rows) stops paying
  * the finished streams' cache reads. */
 int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, void* d_k_cache, void* d_v_cache,
                            int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                            const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B,
                            int H, int D, int L0, const int32_t* d_L0, int cap, int window, int kv_format,
-                           const uint32_t* d_done, int64_t done_stride, void* d_out, int64_t out_stride, float scale,
-                           void* hip_stream);
+                           const uint32_t* d_done, int64_t done_stride, const int32_t* d_stop, void* d_out,
+                           int64_t out_stride, float scale, void* hip_stream);
 
 /* Causal attention over B whole sequences of T tokens (positions 0..T-1, no cache): the prefill of the shared
  * context (code_base/arithmetic.py:115-122, the first call), the guard's scoring forward

@@ -138,7 +138,7 @@ def lib() -> ctypes.CDLL:
                       ctypes.c_float, vp]
     L.ns_decode_attention_ex.restype = ci
     L.ns_decode_attention_ex.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, ci,
-                                         vp, i64, vp, i64, ctypes.c_float, vp]
+                                         vp, i64, vp, vp, i64, ctypes.c_float, vp]
     L.ns_quantize_fp8.restype = ci
     L.ns_quantize_fp8.argtypes = [vp, vp, i64, vp]
     L.ns_lm_gemm.restype = ci

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
                                                           int B, int H, int L0, const int32_t* __restrict__ L0p,
                                                           int cap, int window,
                                                           const uint32_t* __restrict__ done, int64_t done_stride,
+                                                          const int32_t* __restrict__ stop,
                                                           _Float16* __restrict__ out, int64_t out_stride,
                                                           float scale_log2) {
     typedef typename F::Elem E;
@@ -202,9 +203,12 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     for (int rd = 0; rd < rounds; ++rd) {
         const int j = grp + rd * ngrp;
         const int pair = blockIdx.x * P + j;
-        // uniform per wave group; a finished stream (done flag bit 0, e.g. the coder state's NS_ST_DONE) is skipped:
-        // no KV append, no cache read, its output row keeps its old (finite) values, which nothing uses again
-        const bool active = j < P && pair < B * H && !(done && (done[(int64_t)(pair / H) * done_stride] & 1u));
+        // uniform per wave group; a finished stream (done flag bit 0, e.g. the coder state's NS_ST_DONE, or a cache
+        // length at its stop position) is skipped: no KV append, no cache read, its output row keeps its old (finite)
+        // values, which nothing uses again
+        const int sb = pair / H;
+        const bool active = j < P && pair < B * H && !(done && (done[(int64_t)sb * done_stride] & 1u)) &&
+                            !(stop && L0 >= stop[sb]);
         float m = -1e30f, l = 0.0f;
         float acc[DPL];
 #pragma unroll
@@ -530,7 +534,8 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
                             const void* d_k_prefix,
                             const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D, int L0,
                             const int32_t* d_L0, int cap, int window, void* d_out, int64_t out_stride, float scale,
-                            void* hip_stream, const uint32_t* d_done = nullptr, int64_t done_stride = 0) {
+                            void* hip_stream, const uint32_t* d_done = nullptr, int64_t done_stride = 0,
+                            const int32_t* d_stop = nullptr) {
     if (d_done && done_stride < 1) return NS_ERR_CONFIG;
     typedef typename F::Elem E;
     if (window < 0) return NS_ERR_CONFIG;
@@ -574,11 +579,11 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
     if (pairs <= NSG_ATT_SMALL_PAIRS)
         hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 1>), dim3(pairs), dim3(512), 0, st, q, qkv_stride, k, v,
                            cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B, H,
-                           L0, d_L0, cap, window, d_done, done_stride, o, out_stride, scale_log2);
+                           L0, d_L0, cap, window, d_done, done_stride, d_stop, o, out_stride, scale_log2);
     else
         hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 8>), dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k,
                            v, cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B,
-                           H, L0, d_L0, cap, window, d_done, done_stride, o, out_stride, scale_log2);
+                           H, L0, d_L0, cap, window, d_done, done_stride, d_stop, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
@@ -624,18 +629,19 @@ extern "C" int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, voi
                                       int64_t cache_b_stride, int64_t cache_h_stride, int64_t cache_chunk_stride,
                                       const void* d_k_prefix, const void* d_v_prefix, int64_t prefix_h_stride, int T0,
                                       int B, int H, int D, int L0, const int32_t* d_L0, int cap, int window,
-                                      int kv_format, const uint32_t* d_done, int64_t done_stride, void* d_out,
-                                      int64_t out_stride, float scale, void* hip_stream) {
+                                      int kv_format, const uint32_t* d_done, int64_t done_stride,
+                                      const int32_t* d_stop, void* d_out, int64_t out_stride, float scale,
+                                      void* hip_stream) {
     if (kv_format == NS_KV_FP16)
         return decode_attention<nsg::FmtF16>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
                                              cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
                                              d_L0 ? 0 : L0, d_L0, cap, window, d_out, out_stride, scale, hip_stream,
-                                             d_done, done_stride);
+                                             d_done, done_stride, d_stop);
     if (kv_format == NS_KV_FP8)
         return decode_attention<nsg::FmtF8>(d_qkv, qkv_stride, d_k_cache, d_v_cache, cache_b_stride, cache_h_stride,
                                             cache_chunk_stride, d_k_prefix, d_v_prefix, prefix_h_stride, T0, B, H, D,
                                             d_L0 ? 0 : L0, d_L0, cap, window, d_out, out_stride, scale, hip_stream,
-                                            d_done, done_stride);
+                                            d_done, done_stride, d_stop);
     return NS_ERR_CONFIG;
 }
 

@@ -154,7 +154,7 @@ class HipArithmeticLM:
     """Arithmetic-coding provider: batched GPT-2 on PyTorch-ROCm + the HIP coder step."""
 
     decodes_without_state = True  # the interval coder needs no per-token history (unlike the rank coder)
-    skip_done = True  # encode: finished streams skip their decode attention (same tokens; A/B and tests only)
+    skip_done = True  # finished streams skip their attention (encode: done flag, decode: stop position; A/B, tests)
 
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
                  compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096,
@@ -423,18 +423,30 @@ class HipArithmeticLM:
         logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)
         if graphs is None:
             graphs = True
-        if (graphs and sess.T > 2 and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
-                and self.lm.static_capacity_left() >= sess.T):  # replays cannot grow the cache
-            graph = _StepGraph(self.lm, sess.step_static, logits)  # runs token 0, captures the next step
-            for _ in range(1, sess.T):  # the last replay's forward feeds nothing (the cache holds T + 1)
-                graph.replay()
-            del graph
+        native = getattr(self.lm, "native", False) and self.skip_done
+        if native:
+            # the forward after token t feeds token t + 1's logits: a stream of n tokens needs none once the cache
+            # length reaches prefill + n - 1, so its attention is skipped from there (ragged, uneven covers)
+            import torch
+
+            lens = torch.tensor([len(t) for t in token_lists], dtype=torch.int32)
+            self.lm.stop_len = (lens + (self.lm.L - 1)).to(self.lm.device)
+        try:
+            if (graphs and sess.T > 2 and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
+                    and self.lm.static_capacity_left() >= sess.T):  # replays cannot grow the cache
+                graph = _StepGraph(self.lm, sess.step_static, logits)  # runs token 0, captures the next step
+                for _ in range(1, sess.T):  # the last replay's forward feeds nothing (the cache holds T + 1)
+                    graph.replay()
+                del graph
+                return sess.bits()
+            for t in range(sess.T):
+                sess.step(logits)
+                if t + 1 < sess.T:
+                    logits = self.lm.step(sess.tok[t])
             return sess.bits()
-        for t in range(sess.T):
-            sess.step(logits)
-            if t + 1 < sess.T:
-                logits = self.lm.step(sess.tok[t])
-        return sess.bits()
+        finally:
+            if native:
+                self.lm.stop_len = None
 
     def decode_counted(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                        quality: Mapping[str, object], done=None, check_every: int = 64):

@@ -121,6 +121,9 @@ class BatchedGPT2:
         # optional per-stream done flags read by the decode attention (int32 tensor view [B], bit 0 = finished, e.g.
         # the coder state's flags word): finished streams skip their cache reads; their logits are never used again
         self.done_flags = None
+        # optional per-stream stop positions (int32 [B]): a stream whose cache length reached its stop skips its
+        # attention (decode: the position after which its logits are no longer read)
+        self.stop_len = None
         if self.native:
             from .. import _lib
 
@@ -506,6 +509,11 @@ class BatchedGPT2:
         if df is not None and (df.dtype != torch.int32 or df.shape != (B,) or df.device != self.device):
             raise ValueError(f"done_flags must be an int32 [{B}] view on {self.device}")
         done_ptr, done_stride = (df.data_ptr(), df.stride(0)) if df is not None else (None, 0)
+        sl = self.stop_len
+        if sl is not None and (sl.dtype != torch.int32 or sl.shape != (B,) or not sl.is_contiguous()
+                               or sl.device != self.device):
+            raise ValueError(f"stop_len must be a contiguous int32 [{B}] tensor on {self.device}")
+        stop_ptr = sl.data_ptr() if sl is not None else None
         lw0 = self.layers[0]
         ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
                             self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
@@ -527,7 +535,8 @@ class BatchedGPT2:
             rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz,
                             kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
                             kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, self.window,
-                            self._kv_format, done_ptr, done_stride, o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
+                            self._kv_format, done_ptr, done_stride, stop_ptr, o.data_ptr(), o.stride(0),
+                            1.0 / math.sqrt(D), st)
             ok(rc, "ns_decode_attention_prefix")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
             ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)

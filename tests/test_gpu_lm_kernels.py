@@ -634,14 +634,15 @@ def test_decode_attention_done_flags_skip_finished_streams(B, L):
     flags[1::3, 7] = 2  # other bits do not count
     L_ = _lib.lib()
 
-    def run(done):
+    def run(done, stop=None):
         k2, v2 = kc.clone(), vc.clone()
         out = torch.full((B, C), 5.0, device="cuda").half()
         rc = L_.ns_decode_attention_ex(qkv.data_ptr(), qkv.stride(0), k2.data_ptr(), v2.data_ptr(), k2.stride(1),
                                        k2.stride(2), k2.stride(0), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H,
                                        D, L, None, cap, 0, _lib.NS_KV_FP16,
                                        done.data_ptr() if done is not None else None, done.stride(0) if done is not None
-                                       else 0, out.data_ptr(), out.stride(0), 1.0 / math.sqrt(D), _stream_handle())
+                                       else 0, stop.data_ptr() if stop is not None else None, out.data_ptr(),
+                                       out.stride(0), 1.0 / math.sqrt(D), _stream_handle())
         assert rc == 0
         torch.cuda.synchronize()
         return out, k2, v2
@@ -654,6 +655,12 @@ def test_decode_attention_done_flags_skip_finished_streams(B, L):
     r = L - T0  # the appended row of every stream
     assert torch.equal(kg[r // 32, live, :, r % 32], kr[r // 32, live, :, r % 32])
     assert torch.equal(kg[r // 32, ~live, :, r % 32], kc[r // 32, ~live, :, r % 32])  # no append when skipped
+    # stop positions: streams whose stop <= L are skipped the same way
+    stop = torch.full((B,), L + 1, dtype=torch.int32, device="cuda")
+    stop[::2] = L
+    got2, _, _ = run(None, stop)
+    run_s = torch.arange(B, device="cuda") % 2 == 1
+    assert torch.equal(got2[run_s], ref[run_s]) and (got2[~run_s] == 5.0).all()
 
 
 def test_encode_skip_done_streams_gives_the_same_tokens():
