@@ -65,7 +65,7 @@ int64_t ns_frac_scratch_bytes(const ns_frac_ctx* ctx, int nslots, int64_t ld, in
  *   d_probs [B, ld] float64 values and d_ids [B, ld] int32 token ids of the stream's distribution in the
  *   reference's order (array: 0..V-1; dict: sorted keys), d_count[b] = V entries (<= ld);
  *   d_bits [B, bits_stride] the payload, one bit per byte, MSB-first (zero-padded past the payload by the step);
- *   table_limbs: per-stream room for the V + 1 cumulative numerators (NS_FRAC_ERR_CAPACITY if short);
+ *   table_limbs: per-stream room for the V + 1 cumulative numerators (NS_FRAC_ERR_TABLE if short);
  *   max_bits: the largest payload length of the batch (sizes the scratch; at most 2^20 -- NS_ERR_CONFIG above: a
  *   failing step searches one depth per payload bit, each linear in the integers' growing size).
  * Outputs d_token[b] (the token id), d_used[b] (bits consumed = the depth, the reference's history entry). */
