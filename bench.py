@@ -291,7 +291,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
-def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3):
+def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3, T0=32):
     """The decode attention of the headline's step alone (``ns_decode_attention_prefix``, ``decode_attn_kernel``:
     ~80 % of the C3 step): one GPT-2-small layer at the e2e batch, the shared 32-position context stored once and
     each stream's own rows in chunk planes, cache length ``L`` (default: the C3 job's mean attended length), random
@@ -305,7 +305,7 @@ def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3):
     from neuralsteganography_amd import _lib
     from neuralsteganography_amd.coder import _stream_handle
 
-    B, H, D, T0 = args.e2e_batch, 12, 64, 32
+    B, H, D = args.e2e_batch, 12, 64
     C = H * D
     L = int(L or 544)
     rows = L + 1 - T0
@@ -324,7 +324,8 @@ def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3):
 
     def launch():
         rc = lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(1),
-                                            kc.stride(2), kc.stride(0), kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0,
+                                            kc.stride(2), kc.stride(0), kp.data_ptr() if T0 else None,
+                                            vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0,
                                             B, H, D, L, None, T0 + nch * 32, 0, out.data_ptr(), out.stride(0),
                                             1.0 / math.sqrt(D), st)
         if rc != 0:
@@ -586,7 +587,7 @@ def _attn_traffic(args, L):
             continue
         if rec.get("library_version") == ver and rec.get("batch") == args.e2e_batch and rec.get("L"):
             per_row = rec["traffic_bytes_per_launch"] / rec["alg_bytes_per_launch"]
-            B, H, D, T0 = args.e2e_batch, 12, 64, 32
+            B, H, D = args.e2e_batch, 12, 64
             alg = B * H * (L + 1 - T0) * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * H * D * 2 + B * H * D * 2
             return per_row * alg, f"{Path(path).name} (traffic/alg ratio {per_row:.3f} at L = {rec['L']})"
     return None, None

@@ -57,6 +57,12 @@ int ns_lm_gemm_configs(void);
 int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy, int M,
                     int C, float eps, void* hip_stream);
 
+/* ns_lm_layernorm that also advances the int32 *d_counter by one (when not NULL) in the same launch: the decode
+ * step's final layer norm moves the device-side cache length (ns_lm_embed_ln / attention d_L) to the next step
+ * without a launch of its own.  Round 5. */
+int ns_lm_layernorm_count(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
+                          int M, int C, float eps, int32_t* d_counter, void* hip_stream);
+
 /* ns_lm_layernorm of d_x (C = K; ln_w, ln_b) followed by ns_lm_gemm of the normalised rows, in ONE launch when
  * the GEMM is a small-batch one (M <= 16, K <= 1024: every workgroup normalises the M rows into LDS with the
  * layernorm kernel's arithmetic, bit-identical), else the two kernels with d_a fp16 [M, lda] as the normalised

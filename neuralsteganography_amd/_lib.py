@@ -32,6 +32,7 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_read_counters", "ns_decode_attention", "ns_decode_attention_dev", "ns_decode_attention_prefix",
            "ns_decode_attention_fp8", "ns_decode_attention_ex", "ns_quantize_fp8",
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
+           "ns_lm_layernorm_count",
            "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm",
            "ns_frac_create", "ns_frac_destroy", "ns_frac_last_error", "ns_frac_init", "ns_frac_encode_step",
            "ns_frac_decode_step", "ns_frac_set_slots", "ns_frac_scratch_bytes")
@@ -149,6 +150,8 @@ def lib() -> ctypes.CDLL:
     L.ns_lm_gemm_configs.argtypes = []
     L.ns_lm_layernorm.restype = ci
     L.ns_lm_layernorm.argtypes = [vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_lm_layernorm_count.restype = ci
+    L.ns_lm_layernorm_count.argtypes = [vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp, vp]
     L.ns_set_split_max_batch.restype = ci
     L.ns_set_split_max_batch.argtypes = [ci]
     L.ns_lm_embed_ln.restype = ci

@@ -1029,9 +1029,14 @@ __device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, c
     }
 }
 
+// counter (optional): the decode step's device-side cache length, advanced by one thread here -- ln_f runs after
+// every attention layer of the step has read it, and a separate add kernel would cost one more launch per token
+// (graph replays at B = 1 are launch-latency bound)
 __global__ __launch_bounds__(256) void layernorm_kernel(const f16* __restrict__ X, int64_t ldx,
                                                         const f16* __restrict__ w, const f16* __restrict__ b,
-                                                        f16* __restrict__ Y, int64_t ldy, int M, int C, float eps) {
+                                                        f16* __restrict__ Y, int64_t ldy, int M, int C, float eps,
+                                                        int32_t* __restrict__ counter) {
+    if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     const int lane = threadIdx.x & 63, NV4 = C >> 2;
@@ -1377,15 +1382,20 @@ extern "C" int ns_lm_gemm_config(const void* d_x, int64_t ldx, const void* d_wt,
 
 extern "C" int ns_lm_gemm_configs(void) { return CFG_COUNT; }
 
-extern "C" int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
-                               int M, int C, float eps, void* hip_stream) {
+extern "C" int ns_lm_layernorm_count(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y,
+                                     int64_t ldy, int M, int C, float eps, int32_t* d_counter, void* hip_stream) {
     if (!d_x || !d_w || !d_b || !d_y || M <= 0 || C <= 0) return NS_ERR_CONFIG;
     if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
     const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_w | (uintptr_t)d_b | (uintptr_t)d_y;
-    if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C) return NS_ERR_CONFIG;
+    if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C || ((uintptr_t)d_counter & 3u)) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, (const f16*)d_x,
-                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps);
+                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps, d_counter);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_layernorm(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
+                               int M, int C, float eps, void* hip_stream) {
+    return ns_lm_layernorm_count(d_x, ldx, d_w, d_b, d_y, ldy, M, C, eps, nullptr, hip_stream);
 }
 
 extern "C" int ns_lm_ln_gemm(const void* d_x, int64_t ldx, const void* d_lw, const void* d_lb, float eps,

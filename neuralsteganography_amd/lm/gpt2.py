@@ -541,8 +541,9 @@ class BatchedGPT2:
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
             ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)
             gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
-        ok(L.ns_lm_layernorm(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B, C,
-                             eps, st), "ns_lm_layernorm")
+        # ln_f; with a device-side length it also advances d_L for the next step (no launch of its own)
+        ok(L.ns_lm_layernorm_count(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B,
+                                   C, eps, dL, st), "ns_lm_layernorm_count")
         epi = _lib.NS_LM_EPI_STORE_F32 if out.dtype == torch.float32 else _lib.NS_LM_EPI_STORE
         if out.shape != (B, self.ld) or out.stride(1) != 1:
             raise ValueError(f"logits buffer must be [{B}, {self.ld}]")
@@ -568,11 +569,10 @@ class BatchedGPT2:
     @torch.no_grad()
     def step_static(self, tokens: torch.Tensor) -> torch.Tensor:
         """:meth:`step` with every per-step quantity on the device: position ``d_L % n_positions``, the
-        attention's cache length read from ``d_L``, logits written into the fixed buffer, ``d_L += 1``.  Issues
-        no host synchronisation and no allocation that depends on the step, so it can be captured once.  The
-        caller advances the host-side ``L`` by one per executed step."""
+        attention's cache length read from ``d_L``, logits written into the fixed buffer, ``d_L += 1`` (by the
+        final layer norm's launch).  Issues no host synchronisation and no allocation that depends on the step, so
+        it can be captured once.  The caller advances the host-side ``L`` by one per executed step."""
         self._decode_native(tokens, self._static_logits, dev_len=True)
-        self.d_L += 1
         return self._static_logits
 
     @torch.no_grad()

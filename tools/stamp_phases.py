@@ -80,11 +80,14 @@ def main():
             xcd_rows = {}
             for x in range(8):
                 m = xcd == x
+                if not m.any():  # small batches leave XCDs without a stream
+                    continue
                 xcd_rows[x] = {"stream_p50": round(float(np.median(stream_us[m])), 1),
                                "end_p50": round(float(np.median(end_us[m])), 1),
                                "end_max": round(float(end_us[m].max()), 1)}
             slot = (idx % 4)
-            slot_rows = {int(k): round(float(np.median(stream_us[slot == k])), 1) for k in range(4)}
+            slot_rows = {int(k): round(float(np.median(stream_us[slot == k])), 1) for k in range(4)
+                         if (slot == k).any()}
             print(json.dumps({"per_xcd": xcd_rows, "stream_p50_by_wave_slot": slot_rows}), file=sys.stderr)
         if t == 2:
             print(f"valid rows {int(ok.sum())}; median clock {np.median(ticks_per_us):.1f} ticks/us", file=sys.stderr)
