@@ -235,6 +235,19 @@ def fraction_coder(args, rank, world, dev):
                         "host-inclusive lockstep encode"}
 
 
+def _wide_traffic(B):
+    """HBM bytes per wide_onepass_kernel launch from the committed PMC passes (profiles/r05/
+    pmc_traffic_wide_onepass_f32_v017.json: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), scaled to batch B,
+    or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05",
+                        "pmc_traffic_wide_onepass_f32_v017.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return rec["traffic_bytes_per_launch"] * B / rec["batch"]
+
+
 def wide_path(args, rank, world, dev, steps=10, warmup=3):
     """The api default quality (precision 16, topk 50,000: api.py:81-86) at the coder batch: the wide path
     (csrc/nsg_wide.hip) on resident 3*N(0,1) fp32 logits, 1-KiB payloads, whole steps timed with HIP events on
@@ -287,6 +300,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
             "achieved_gbs": alg / (el_max / steps) / 1e9, "peak_gbs": HBM_PEAK_GBS,
             "frac": alg / (el_max / steps) / 1e9 / HBM_PEAK_GBS,
             "listed_stream_step_fraction": (c1[0] - c0[0]) / max(ntok, 1),
+            "traffic": _wide_traffic(B),
             "workload": f"api default quality: {B} streams/GPU x ns_encode_step, precision 16, topk 50000, temp 1.0, "
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
