@@ -190,6 +190,34 @@ def test_layernorm_matches_torch(M, C):
     assert torch.equal(y1[0], y[0])
 
 
+@pytest.mark.parametrize("M", [1, 9, 4096])
+def test_layernorm_count_advances_the_counter_once(M):
+    """ns_lm_layernorm_count (the decode step's ln_f in a captured graph) writes the same rows as
+    ns_lm_layernorm and adds exactly one to the device counter, whatever the grid size."""
+    C = 768
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.randn((M, C), generator=g, device="cuda").half()
+    w = torch.randn((C,), generator=g, device="cuda").half()
+    b = torch.randn((C,), generator=g, device="cuda").half()
+    y0 = torch.empty((M, C), device="cuda").half()
+    y1 = torch.empty((M, C), device="cuda").half()
+    ctr = torch.tensor([41], dtype=torch.int32, device="cuda")
+    L = _lib.lib()
+    assert L.ns_lm_layernorm(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y0.data_ptr(), C, M, C, 1e-5,
+                             _stream_handle()) == 0
+    for _ in range(3):
+        assert L.ns_lm_layernorm_count(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y1.data_ptr(), C, M, C, 1e-5,
+                                       ctr.data_ptr(), _stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert int(ctr.item()) == 44
+    # no counter: plain layer norm
+    assert L.ns_lm_layernorm_count(x.data_ptr(), C, w.data_ptr(), b.data_ptr(), y1.data_ptr(), C, M, C, 1e-5,
+                                   None, _stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert int(ctr.item()) == 44
+
+
 @pytest.mark.parametrize("dev_len", [False, True])
 def test_embed_ln_matches_torch(dev_len):
     V, P, C, M, L = 1000, 64, 256, 9, 70  # position = 70 % 64 = 6
