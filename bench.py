@@ -236,16 +236,22 @@ def fraction_coder(args, rank, world, dev):
 
 
 def _wide_traffic(B):
-    """HBM bytes per wide_onepass_kernel launch from the committed PMC passes (profiles/r05/
-    pmc_traffic_wide_onepass_f32_v017.json: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), scaled to batch B,
-    or None."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05",
-                        "pmc_traffic_wide_onepass_f32_v017.json")
-    try:
-        rec = json.load(open(path))
-    except (OSError, ValueError):
-        return None
-    return rec["traffic_bytes_per_launch"] * B / rec["batch"]
+    """HBM bytes per wide_onepass_kernel launch from a committed PMC record of THIS library build
+    (profiles/r05/pmc_traffic_wide_onepass_*.json: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), scaled to
+    batch B, or None."""
+    import glob
+
+    from neuralsteganography_amd import _lib
+
+    ver = _lib.version()
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_wide_onepass_*.json"))):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if rec.get("library_version") == ver:
+            return rec["traffic_bytes_per_launch"] * B / rec["batch"]
+    return None
 
 
 def wide_path(args, rank, world, dev, steps=10, warmup=3):

@@ -743,9 +743,9 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 // canonical tail on the sorted keys: the same arithmetic, in the same order, as wide_cdf_kernel.  Streams that
 // need the exact row sum, the row-statistics fallback, the sampler, or hit an error are handed to
 // wide_cdf_kernel (listed in todo) with their sorted keys written to keys_out; streams with more keys were
-// sorted by the device-wide sort and are listed too.  53,248 B of LDS and <= 80 VGPRs: three workgroups per
-// CU (measured 0.53 vs 0.58 ms per step with 8,192 keys / 3,840 buckets at two per CU: more rows in flight while
-// other workgroups run their latency-bound tails).
+// sorted by the device-wide sort and are listed too.  Round 3-4: 53,248 B of LDS and <= 80 VGPRs, three
+// workgroups per CU (measured 0.53 vs 0.58 ms per step with 8,192 keys / 3,840 buckets at two per CU, an older
+// kernel); round 5: two per CU without the spill frame (NSG_FAST_WAVES_PER_SIMD below).
 #ifndef NSG_SCAN_DIAG
 #define NSG_SCAN_DIAG 0
 #endif
@@ -758,13 +758,16 @@ __global__ __launch_bounds__(WIDE_THREADS) void wide_cdf_kernel(StepParams p, co
 constexpr int FAST_THREADS = 512;
 constexpr int FAST_WAVES = FAST_THREADS / WAVE;
 #ifndef NSG_FAST_NL
-#define NSG_FAST_NL 5632
+#define NSG_FAST_NL 6144  // round 5 (two workgroups per CU leave the LDS for it): 5,632 before
 #endif
 #ifndef NSG_FAST_NB
 #define NSG_FAST_NB 2048
 #endif
 #ifndef NSG_FAST_WAVES_PER_SIMD
-#define NSG_FAST_WAVES_PER_SIMD 6  // launch-bounds occupancy target: 6 = three 512-thread workgroups per CU
+// launch-bounds occupancy target.  Round 5: 4 = two 512-thread workgroups per CU, 127 VGPRs and 36 B of scratch per
+// lane, against 6 = three per CU at 80 VGPRs, whose ~200-byte spill frame per lane was 410 MB of HBM writes per
+// launch (PMC 1.85x the algorithmic bytes -> 1.08x) -- and 3.5-4 % faster (profiles/r05/wide_occupancy_ab/)
+#define NSG_FAST_WAVES_PER_SIMD 4
 #endif
 constexpr int FAST_NL = NSG_FAST_NL;               // keys of a stream sorted in LDS
 constexpr int FAST_R = FAST_NL / FAST_THREADS;     // ranks per thread: rank i = r * FAST_THREADS + tid
