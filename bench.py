@@ -607,7 +607,7 @@ def _attn_traffic(args, L):
             continue
         if rec.get("library_version") == ver and rec.get("batch") == args.e2e_batch and rec.get("L"):
             per_row = rec["traffic_bytes_per_launch"] / rec["alg_bytes_per_launch"]
-            B, H, D = args.e2e_batch, 12, 64
+            B, H, D, T0 = args.e2e_batch, 12, 64, 32
             alg = B * H * (L + 1 - T0) * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * H * D * 2 + B * H * D * 2
             return per_row * alg, f"{Path(path).name} (traffic/alg ratio {per_row:.3f} at L = {rec['L']})"
     return None, None
