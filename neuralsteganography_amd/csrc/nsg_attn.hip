@@ -26,6 +26,11 @@ namespace nsg {
 #ifndef NSG_ATT_ROWS1
 #define NSG_ATT_ROWS1 256  // keys per pair up to which one wave takes the whole pair (then 2, 4, 8 waves)
 #endif
+#ifndef NSG_ATT_HEAD_MAJOR
+#define NSG_ATT_HEAD_MAJOR 1  // large batches: a workgroup's 8 pairs are 8 streams of ONE head (shared context rows
+                              // then come from the CU's cache), not 8 consecutive (stream, head) pairs; round 5:
+                              // 0.2-1.3 % faster at L = 300-1,000 (profiles/r05/attn_head_major_ab/)
+#endif
 #ifndef NSG_ATT_SMALL_PAIRS
 #define NSG_ATT_SMALL_PAIRS 1024  // up to this many (stream, head) pairs: one pair per workgroup
 #endif
@@ -161,6 +166,18 @@ struct FmtF8 {
 // Positions [0, T0) come from a prefix shared by every stream (kp/vp, head stride ph: the common context,
 // stored once), positions [T0, L0] from the stream's own cache at index position - T0.  Same values, same
 // order: the output bits do not depend on where a row is stored.
+// Which (stream, head) pair slot j of workgroup g serves (-1: none).  Work placement only: the math of a pair does
+// not depend on it.
+template <int P>
+__device__ __forceinline__ int att_pair(int g, int j, int B, int H) {
+    if (P > 1 && NSG_ATT_HEAD_MAJOR) {
+        const int h = g % H, b = (g / H) * P + j;
+        return b < B ? b * H + h : -1;
+    }
+    const int pair = g * P + j;
+    return pair < B * H ? pair : -1;
+}
+
 template <class F, int P>
 __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __restrict__ qkv, int64_t qkv_stride,
                                                           typename F::Elem* kc, typename F::Elem* vc, int64_t cb,
@@ -180,8 +197,8 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
         // the host cannot see an overflow before the launch, so poison this workgroup's output rows: the NaNs
         // reach the logits and the coder rejects them, instead of the next GEMM reusing stale rows
         for (int i = threadIdx.x; i < P * ATT_D; i += blockDim.x) {
-            const int pair = blockIdx.x * P + i / ATT_D;
-            if (pair < B * H)
+            const int pair = att_pair<P>(blockIdx.x, i / ATT_D, B, H);
+            if (pair >= 0)
                 out[(int64_t)(pair / H) * out_stride + (pair % H) * ATT_D + i % ATT_D] = (_Float16)__builtin_nanf("");
         }
         return;
@@ -202,12 +219,12 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     const int rounds = (P + ngrp - 1) / ngrp;
     for (int rd = 0; rd < rounds; ++rd) {
         const int j = grp + rd * ngrp;
-        const int pair = blockIdx.x * P + j;
+        const int pair = j < P ? att_pair<P>(blockIdx.x, j, B, H) : -1;
         // uniform per wave group; a finished stream (done flag bit 0, e.g. the coder state's NS_ST_DONE, or a cache
         // length at its stop position) is skipped: no KV append, no cache read, its output row keeps its old (finite)
         // values, which nothing uses again
         const int sb = pair / H;
-        const bool active = j < P && pair < B * H && !(done && (done[(int64_t)sb * done_stride] & 1u)) &&
+        const bool active = pair >= 0 && !(done && (done[(int64_t)sb * done_stride] & 1u)) &&
                             !(stop && L0 >= stop[sb]);
         float m = -1e30f, l = 0.0f;
         float acc[DPL];
@@ -581,7 +598,8 @@ static int decode_attention(const void* d_qkv, int64_t qkv_stride, void* d_k_cac
                            cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B, H,
                            L0, d_L0, cap, window, d_done, done_stride, d_stop, o, out_stride, scale_log2);
     else
-        hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 8>), dim3((pairs + 7) / 8), dim3(512), 0, st, q, qkv_stride, k,
+        hipLaunchKernelGGL((nsg::decode_attn_kernel<F, 8>), dim3(NSG_ATT_HEAD_MAJOR ? H * ((B + 7) / 8) : (pairs + 7) / 8),
+                           dim3(512), 0, st, q, qkv_stride, k,
                            v, cache_b_stride, cache_h_stride, cache_chunk_stride, kp, vp, prefix_h_stride, T0, B,
                            H, L0, d_L0, cap, window, d_done, done_stride, d_stop, o, out_stride, scale_log2);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
