@@ -85,19 +85,17 @@ def parse(argv=None):
                     help="skip the trained-entropy side line (GPT-2-small head scaled so rows carry a few bits/token)")
     ap.add_argument("--trained-scale", type=float, default=6.0, help="head scale (6: ~4.2 bits/token)")
     ap.add_argument("--trained-payload-bytes", type=int, default=512)
-    ap.add_argument("--trained-batch", type=int, default=1024,
-                    help="streams of the trained-entropy leg (covers ~2x as long as C3's on average, and a few far "
-                         "longer: the KV cache is sized for the longest)")
+    ap.add_argument("--trained-messages", type=int, default=16384,
+                    help="trained-entropy leg: messages per GPU, queued through --trained-batch slots")
+    ap.add_argument("--trained-batch", type=int, default=4096,
+                    help="slots of the trained-entropy leg (covers ~2x as long as C3's on average, a few far longer: "
+                         "finished slots take the next queued message)")
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the batch-1 end-to-end side line (BASELINE config C2: GPT-2-small, B = 1, 1 KiB payload)")
     ap.add_argument("--e2e-batch", type=int, default=4096)
     ap.add_argument("--e2e-model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-fa"])
     ap.add_argument("--e2e-payload-bytes", type=int, default=1024)
     ap.add_argument("--e2e-eager", action="store_true", help="per-token launches instead of the captured hipGraph")
-    ap.add_argument("--e2e-kv-layout", default="chunked", choices=["chunked", "plain"],
-                    help="KV cache layout of the native decode step (A/B)")
-    ap.add_argument("--e2e-kv-cap", type=int, default=None,
-                    help="cap the initial per-stream KV cache length (positions; it still grows on demand)")
     ap.add_argument("--blas", default=None, choices=["rocblas", "hipblaslt"],
                     help="GEMM library for the GPT-2 forward (torch.backends.cuda.preferred_blas_library)")
     ap.add_argument("--e2e-logits", default="f16", choices=["f32", "f16"],
@@ -386,7 +384,7 @@ def rank_payloads(total, world, rank, nbytes):
     return [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, nbytes)) for s in shard_range(total, world, rank)]
 
 
-def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=None):
+def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=None, slots=None):
     """One timed whole job on this rank: ``lm.encode_batch`` of the rank's streams to completion, bracketed by a
     barrier and a device synchronisation on both sides; then (``decode``) ``lm.decode_batch`` of the covers,
     timed the same way, and the share of streams whose payload came back bit for bit.  Totals are summed over
@@ -413,7 +411,8 @@ def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=
             dist.barrier()
         return res, dt
 
-    toks, elapsed = timed(lambda: lm.encode_batch(bit_lists, context, quality=quality, graphs=graphs))
+    kw = {"slots": slots} if slots else {}
+    toks, elapsed = timed(lambda: lm.encode_batch(bit_lists, context, quality=quality, graphs=graphs, **kw))
     nbits = sum(len(b) for b in bit_lists)
     ntok = sum(len(t) for t in toks)
     steps = max((len(t) for t in toks), default=0)
@@ -426,7 +425,7 @@ def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=
            "lockstep_steps": int(steps_max), "ms_per_step": 1e3 * el_max / max(steps_max, 1),
            "bits_per_token": bits_all / max(tok_all, 1)}
     if decode:
-        dec, dt = timed(lambda: lm.decode_batch(toks, context, quality=quality, graphs=graphs))
+        dec, dt = timed(lambda: lm.decode_batch(toks, context, quality=quality, graphs=graphs, **kw))
         exact = sum(1 for d, b in zip(dec, bit_lists) if list(d[: len(b)]) == list(b))
         ex_all, n_all, dt_max, _ = reduce_job(exact, len(bit_lists), dt, 0.0, device=dev)
         out["roundtrip_exact_fraction"] = ex_all / max(n_all, 1)
@@ -438,7 +437,7 @@ def e2e_job(lm, bit_lists, context, quality, *, dev, world, decode=True, graphs=
 
 
 def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, model=None, topk=None,
-               decode=False, logit_scale=1.0, payload_bytes=None):
+               decode=False, logit_scale=1.0, payload_bytes=None, messages=None, slots=None):
     """The whole stego encode at batch: GPT-2 forward (random-init weights of the named architecture, fp16
     compute, HIP decode step) + HIP coder step per token, every stream encoding its full payload from the shared
     32-token context until the last stream is done (lockstep, like the reference's per-message loop run for all
@@ -457,28 +456,27 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
         torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}[args.blas])
     lm = HipArithmeticLM(random_gpt2(model), None, device=str(dev), logits_dtype=args.e2e_logits,
                          max_batch=B, kv_dtype=kv_dtype, attention_window=window, logit_scale=logit_scale)
-    lm.lm.position_cap = args.e2e_kv_cap
-    lm.lm.chunked_cache = args.e2e_kv_layout == "chunked"
     quality = {"temp": args.temp, "precision": args.precision, "topk": topk}
     # [<|endoftext|>] + 31 ids; the end-of-text id is the vocabulary's last (gpt2-fa: 42,000)
     context = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     graphs = False if args.e2e_eager else None
-    # warm-up: kernels and the coder context at the same batch, short payloads; then the full-size KV cache is
-    # allocated and written once (a fresh process's first pass over ~250 GB of new allocations measured up to
-    # 12 % slower per step than later ones), and handed back to PyTorch's caching allocator for the timed run
-    lm.encode_batch([[1, 0, 1, 1] * 8] * B, context, quality=quality, graphs=graphs)
-    bits = rank_payloads(B * world, world, rank, nbytes)
-    lm.lm.prefill(context, B, 2 * max(len(b) for b in bits) + 64)
-    lm.lm.k_cache.zero_()
-    lm.lm.v_cache.zero_()
-    lm.lm.k_cache = lm.lm.v_cache = None
+    # warm-up: kernels and the coder context at the same batch, short payloads; then the KV page pool is grown to
+    # what the device allows and written once (a fresh process's first pass over ~250 GB of new allocations
+    # measured up to 12 % slower per step than later ones): the timed job maps warm pages, allocates none
+    S = min(B, slots or B)
+    lm.encode_batch([[1, 0, 1, 1] * 8] * S, context, quality=quality, graphs=graphs)
+    msgs = messages or B
+    bits = rank_payloads(msgs * world, world, rank, nbytes)
+    pool_pages = lm.lm.warm_pool(B=S)
     torch.cuda.synchronize()
-    out = e2e_job(lm, bits, context, quality, dev=dev, world=world, decode=decode, graphs=graphs)
-    out.update({"kv_positions": lm.lm.max_len, "kv_dtype": kv_dtype, "attention_window": window or None,
+    out = e2e_job(lm, bits, context, quality, dev=dev, world=world, decode=decode, graphs=graphs, slots=S)
+    out.update({"kv_pages_pool": pool_pages, "kv_page_bytes": lm.lm.pool.page_bytes, "schedule": lm.last_schedule,
+                "kv_dtype": kv_dtype, "attention_window": window or None,
                 "workload": f"{model} (random-init weights, fp16 compute, {args.e2e_logits} logits, {kv_dtype} KV "
                             f"cache, batch-invariant native decode step) + ns_encode_step (temp {args.temp}, "
-                            f"precision {args.precision}, topk {topk}), {B} streams/GPU x {nbytes}-"
-                            f"byte payloads encoded to completion from a 32-token context, "
+                            f"precision {args.precision}, topk {topk}), {msgs} messages/GPU x {nbytes}-"
+                            f"byte payloads through {S} slots (paged KV cache, slot refill), encoded to completion "
+                            f"from a 32-token context, "
                             + (f"head scaled x{logit_scale} (trained-entropy rows), " if logit_scale != 1.0 else "")
                             + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")})
     del lm
@@ -832,7 +830,7 @@ def main():
         log("trained-entropy end to end")
         side["end_to_end_trained"] = _side_leg(lambda: end_to_end(
             args, rank, world, dev, decode=True, logit_scale=args.trained_scale, batch=args.trained_batch,
-            payload_bytes=args.trained_payload_bytes))
+            payload_bytes=args.trained_payload_bytes, messages=args.trained_messages, slots=args.trained_batch))
     roofline_attn = None
     if not args.no_e2e and not args.no_attention_bench:
         # the decode attention at the C3 job's mean attended length: T0 + (lockstep steps + 1) / 2 keys

@@ -79,6 +79,17 @@ int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe
                    const int32_t* d_L, void* d_h, int64_t ldh, const void* d_w, const void* d_b, void* d_a,
                    int64_t lda, int M, int C, float eps, void* hip_stream);
 
+/* ns_lm_embed_ln with a cache length PER ROW: row b takes position d_lens[b] mod n_positions (int32 [M], device;
+ * code_base/arithmetic.py:44-48 per message).  The paged decode step with slot refill (round 6). */
+int ns_lm_embed_ln_rows(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions,
+                        const int32_t* d_lens, void* d_h, int64_t ldh, const void* d_w, const void* d_b, void* d_a,
+                        int64_t lda, int M, int C, float eps, void* hip_stream);
+
+/* ns_lm_layernorm that also advances d_lens[row] by one for every row (int32 [M]) in the same launch: the paged
+ * decode step's ln_f moves every stream's cache length after all its attention layers have read it. */
+int ns_lm_layernorm_rows(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y, int64_t ldy,
+                         int M, int C, float eps, int32_t* d_lens, void* hip_stream);
+
 /* ns_lm_embed_ln for M = B*T rows of whole sequences: row b*T + t takes position t mod n_positions (the default
  * positions of a first forward call: the context prefill, the guard's scoring forward, the max_context window). */
 int ns_lm_embed_seq_ln(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions, int T,

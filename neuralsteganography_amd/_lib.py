@@ -34,6 +34,7 @@ EXPORTS = ("ns_create", "ns_destroy", "ns_last_error", "ns_version", "ns_max_top
            "ns_score_rows", "ns_lm_gemm", "ns_lm_gemm_config", "ns_lm_gemm_configs", "ns_lm_layernorm",
            "ns_lm_layernorm_count",
            "ns_lm_embed_ln", "ns_lm_embed_seq_ln", "ns_seq_attention", "ns_lm_ln_gemm",
+           "ns_decode_attention_paged", "ns_lm_embed_ln_rows", "ns_lm_layernorm_rows",
            "ns_frac_create", "ns_frac_destroy", "ns_frac_last_error", "ns_frac_init", "ns_frac_encode_step",
            "ns_frac_decode_step", "ns_frac_set_slots", "ns_frac_scratch_bytes")
 NS_LM_EPI_STORE, NS_LM_EPI_GELU, NS_LM_EPI_RESIDUAL, NS_LM_EPI_STORE_F32 = 0, 1, 2, 3
@@ -140,6 +141,13 @@ def lib() -> ctypes.CDLL:
     L.ns_decode_attention_ex.restype = ci
     L.ns_decode_attention_ex.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, ci,
                                          vp, i64, vp, vp, i64, ctypes.c_float, vp]
+    L.ns_decode_attention_paged.restype = ci
+    L.ns_decode_attention_paged.argtypes = [vp, i64, vp, i64, ci, ci, vp, vp, i64, ci, ci, ci, ci, vp, ci, ci, vp, i64,
+                                            vp, vp, i64, ctypes.c_float, vp]
+    L.ns_lm_embed_ln_rows.restype = ci
+    L.ns_lm_embed_ln_rows.argtypes = [vp, vp, vp, ci, ci, vp, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]
+    L.ns_lm_layernorm_rows.restype = ci
+    L.ns_lm_layernorm_rows.argtypes = [vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp, vp]
     L.ns_quantize_fp8.restype = ci
     L.ns_quantize_fp8.argtypes = [vp, vp, i64, vp]
     L.ns_lm_gemm.restype = ci

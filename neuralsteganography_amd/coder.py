@@ -285,7 +285,7 @@ class EncodeSession:
     tolerance of the reference, not bit-exact -- at the cost of a heavier kernel build."""
 
     def __init__(self, ctx: CoderContext, payload_bits: Sequence[Sequence[int]], max_tokens: Optional[int] = None,
-                 stats: bool = False):
+                 stats: bool = False, payload_stride: Optional[int] = None):
         torch = _torch()
         self.ctx = ctx
         self.B = len(payload_bits)
@@ -293,7 +293,7 @@ class EncodeSession:
             raise ConfigurationError(f"batch {self.B} outside [1, {ctx.max_batch}]")
         dev = torch.device("cuda", ctx.device)
         self.nbits_host = np.asarray([len(b) for b in payload_bits], dtype=np.int64)
-        stride = max(1, int((self.nbits_host.max() + 7) // 8))
+        stride = max(1, int((self.nbits_host.max() + 7) // 8), int(payload_stride or 0))
         pl = np.zeros((self.B, stride), dtype=np.uint8)
         for i, bits in enumerate(payload_bits):
             if len(bits):
@@ -372,6 +372,59 @@ class EncodeSession:
 
     def fields(self) -> dict:
         return _state_fields(self.state)
+
+    # ---------------------------------------------------------------- slots (lm/slots.py: refill, compaction)
+    def load_slots(self, slots: Sequence[int], payload_bits: Sequence[Sequence[int]]) -> None:
+        """Start new payloads in ``slots`` (rows of this session): payload row, bit count, a fresh coder state
+        (``ns_init_state``'s values) and, with stats, zeroed accumulators.  The token history row is reused from
+        position 0 (only the first ``ntokens`` entries of a row are ever read)."""
+        torch = _torch()
+        n = len(slots)
+        if n == 0:
+            return
+        stride = self.payload.shape[1]
+        pl = np.zeros((n, stride), dtype=np.uint8)
+        nb = np.zeros(n, dtype=np.int64)
+        for i, bits in enumerate(payload_bits):
+            nb[i] = len(bits)
+            if len(bits):
+                packed = np.packbits(_bit_array(bits), bitorder="little")
+                if packed.size > stride:
+                    raise ConfigurationError("payload longer than the session's payload stride")
+                pl[i, : packed.size] = packed
+        dev = self.state.device
+        idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=dev)
+        self.payload[idx] = torch.from_numpy(pl).to(dev)
+        self.nbits[idx] = torch.from_numpy(nb).to(dev)
+        self.nbits_host[np.asarray(slots)] = nb
+        self.state[idx] = self.init_row().expand(n, 4)
+        if self.stats_acc is not None:
+            self.stats_acc[idx] = 0
+
+    def init_row(self):
+        """[1, 4] int64: the state ``ns_init_state`` writes (lo 0, hi 2^precision, bit_pos 0, ntokens | flags 0)."""
+        torch = _torch()
+        return torch.tensor([[0, 1 << self.ctx.params.precision, 0, 0]], dtype=torch.int64, device=self.state.device)
+
+    def park_slots(self, slots: Sequence[int]) -> None:
+        """Mark ``slots`` finished (NS_ST_DONE): the coder step and the decode attention skip them (empty slots)."""
+        if len(slots) == 0:
+            return
+        torch = _torch()
+        idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=self.state.device)
+        w = self.state.view(torch.int32)
+        w[idx, 7] = w[idx, 7] | _lib.NS_ST_DONE
+
+    def compact(self, keep: Sequence[int]) -> None:
+        """Keep rows ``keep`` (in that order) of every per-stream buffer: the session now has len(keep) streams."""
+        torch = _torch()
+        idx = torch.as_tensor(np.asarray(keep, dtype=np.int64), device=self.state.device)
+        for name in ("payload", "nbits", "state", "out_token", "hist", "stats_acc", "trace"):
+            t = getattr(self, name)
+            if t is not None:
+                setattr(self, name, t.index_select(0, idx).contiguous())
+        self.nbits_host = self.nbits_host[np.asarray(keep, dtype=np.int64)]
+        self.B = len(keep)
 
     def raise_errors(self) -> None:
         f = self.fields()["flags"]

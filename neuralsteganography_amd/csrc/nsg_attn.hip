@@ -412,6 +412,299 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(const _Float16* __rest
     }
 }
 
+// ------------------------------------------------------------------------------------------------- paged KV
+// The same attention over a PAGED cache with a cache length PER STREAM (include/nsg_attn.h,
+// ns_decode_attention_paged).  A stream's rows live in 32-position pages it owns: d_table[b][c] is the device
+// address of the page holding stream rows 32c..32c+31 (positions T0 + 32c ...), a page laid out [layer][K|V][H][32]
+// [D], so growth only maps new pages (no copy, no second cache) and a finished stream's pages go to the next message
+// (slot refill, reference: every message runs its own loop with its own cache, code_base/arithmetic.py:96-122).
+//
+// With per-stream lengths the row split S of a pair (att_split of its own key count) differs inside a workgroup, so
+// the work is cut into TASKS: task (pair j, split w) streams rows s0 + 32w, s0 + 32(w + S), ... exactly as wave w of
+// the lockstep kernel does, the 8 waves take the tasks round-robin, every task's partial goes to LDS, and wave j then
+// merges pair j's S partials in split order with the lockstep kernel's arithmetic (an S = 1 "merge" is exact: *1,
+// +0).  Same rows, same order, same operations: the output bits equal the lockstep kernel's for the same cache
+// contents, and still depend on a pair's own key count only (batch-invariant).
+struct PagedArgs {
+    const _Float16* qkv;
+    int64_t qkv_stride;
+    const uint64_t* table;  // [B][tstride] page addresses (bytes), 0 = no page
+    int64_t tstride;
+    int max_chunks;         // table entries per stream in use
+    int64_t layer_off;      // elements from a page's base to this layer's K block ([layer][K|V][H][32][D])
+    int64_t v_off;          // elements from the K block to the V block (H * 32 * D)
+    const void* kp;         // shared prefix [H][ph] (positions < T0), fp16 or fp8 like the pages
+    const void* vp;
+    int64_t ph;
+    int T0, B, H;
+    const int32_t* lens;    // [B] positions already cached per stream (the new token goes to position lens[b])
+    int window;
+    const uint32_t* done;
+    int64_t done_stride;
+    const int32_t* stop;
+    _Float16* out;
+    int64_t out_stride;
+    float scale_log2;
+};
+
+template <class F, int P>
+__global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
+    typedef typename F::Elem E;
+    typedef typename F::Raw Raw;
+    constexpr int DPL = F::DPL, LPR = F::LPR, RPI = F::RPI, NI = F::NI;
+    constexpr int NT = 8 * P;  // at most 8 splits per pair
+    __shared__ float s_m[NT], s_l[NT];
+    __shared__ float s_acc[NT][ATT_D];
+    __shared__ int s_info[P][6];  // pair, L0, s0, S, first task, status (0 none / skipped, 1 run, 2 poison)
+    __shared__ int s_ntask;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (wave == 0) {  // lane j < P: pair j's length, skip flags and split; an exclusive prefix sum gives its tasks
+        int pair = -1, L0 = 0, s0 = 0, S = 0, st = 0;
+        if (lane < P) {
+            pair = att_pair<P>(blockIdx.x, lane, a.B, a.H);
+            if (pair >= 0) {
+                const int b = pair / a.H;
+                L0 = a.lens[b];
+                const bool skip = (a.done && (a.done[(int64_t)b * a.done_stride] & 1u)) || (a.stop && L0 >= a.stop[b]);
+                if (!skip) {
+                    const int jj = L0 - a.T0;  // the new token's stream row: its page must exist (host invariant)
+                    const uint64_t pg = (jj >= 0 && (jj >> 5) < a.max_chunks) ? a.table[(int64_t)b * a.tstride + (jj >> 5)]
+                                                                               : 0;
+                    if (pg == 0 || (pg & 15u)) {
+                        st = 2;  // no page: poison the output (NaN logits the coder rejects), never write
+                    } else {
+                        st = 1;
+                        const int Lk = L0 + 1;
+                        s0 = a.window > 0 ? max(0, Lk - a.window) : 0;
+                        S = att_split(Lk - s0);
+                    }
+                }
+            }
+        }
+        int first = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int sk = __shfl(S, k);
+            first += k < lane ? sk : 0;
+            total += sk;
+        }
+        if (lane < P) {
+            s_info[lane][0] = pair;
+            s_info[lane][1] = L0;
+            s_info[lane][2] = s0;
+            s_info[lane][3] = S;
+            s_info[lane][4] = first;
+            s_info[lane][5] = st;
+        }
+        if (lane == 0) s_ntask = total;
+    }
+    __syncthreads();
+    const int ntask = s_ntask;
+    const int g = lane / LPR;  // row within an RPI-row slab
+    const int c = lane % LPR;  // DPL-dim slice
+    const int C = a.H * ATT_D;
+    for (int t = wave; t < ntask; t += 8) {  // wave-uniform
+        int j = 0;
+#pragma unroll
+        for (int k = 1; k < P; ++k)
+            if (t >= s_info[k][4] && s_info[k][3] > 0) j = k;
+        const int pair = __builtin_amdgcn_readfirstlane(s_info[j][0]);
+        const int L0 = __builtin_amdgcn_readfirstlane(s_info[j][1]);
+        const int s0 = __builtin_amdgcn_readfirstlane(s_info[j][2]);
+        const int S = __builtin_amdgcn_readfirstlane(s_info[j][3]);
+        const int wv = t - __builtin_amdgcn_readfirstlane(s_info[j][4]);
+        const int T0 = a.T0;
+        const int Lk = L0 + 1;
+        const int last_cached = L0 > 0 ? L0 - 1 : 0;
+        const int b = pair / a.H, h = pair - b * a.H;
+        const uint64_t* trow = a.table + (int64_t)b * a.tstride;
+        const _Float16* qrow = a.qkv + (int64_t)b * a.qkv_stride + h * ATT_D + c * DPL;
+        const typename F::Q q = F::load_q(qrow);
+        const Raw knew = F::from_qkv(qrow + C);
+        const Raw vnew = F::from_qkv(qrow + 2 * C);
+        const int64_t hoff = a.layer_off + (int64_t)h * 32 * ATT_D + c * DPL;  // this layer's K rows of head h
+        auto kaddr = [&](uint64_t page, int jj) -> E* { return (E*)page + hoff + (int64_t)(jj & 31) * ATT_D; };
+        const E* kpb = (const E*)a.kp + (int64_t)h * a.ph + c * DPL;
+        const E* vpb = (const E*)a.vp + (int64_t)h * a.ph + c * DPL;
+        if (g == 0 && wv == 0) {  // KV append of the new token (position L0, page checked above)
+            E* kd = kaddr(trow[(L0 - T0) >> 5], L0 - T0);
+            *(Raw*)kd = knew;
+            *(Raw*)(kd + a.v_off) = vnew;
+        }
+        float m = -1e30f, l = 0.0f;
+        float acc[DPL];
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) acc[d] = 0.0f;
+        // one iteration = RPI*NI = 32 consecutive rows from j0; GENERAL handles the prefix boundary, the clamp past
+        // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages, looked up
+        // once per iteration (wave-uniform)
+        auto load_chunk = [&](int j0, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
+            constexpr bool GEN = decltype(general)::value;
+            if constexpr (GEN) {
+#pragma unroll
+                for (int u = 0; u < NI; ++u) {
+                    const int row = min(j0 + RPI * u + g, last_cached);
+                    if (row < T0) {
+                        kr[u] = att_load((const Raw*)(kpb + (int64_t)row * ATT_D));
+                        vr[u] = att_load((const Raw*)(vpb + (int64_t)row * ATT_D));
+                    } else {
+                        const E* ka = kaddr(trow[(row - T0) >> 5], row - T0);
+                        kr[u] = att_load((const Raw*)ka);
+                        vr[u] = att_load((const Raw*)(ka + a.v_off));
+                    }
+                }
+            } else {
+                const int jj0 = j0 - T0;
+                const int ca = jj0 >> 5;
+                const uint64_t pa = trow[ca];
+                const uint64_t pb = (jj0 & 31) ? trow[ca + 1] : pa;
+#pragma unroll
+                for (int u = 0; u < NI; ++u) {
+                    const int jj = jj0 + RPI * u + g;
+                    const E* ka = kaddr((jj >> 5) == ca ? pa : pb, jj);
+                    kr[u] = att_load((const Raw*)ka);
+                    vr[u] = att_load((const Raw*)(ka + a.v_off));
+                }
+            }
+        };
+        auto math_chunk = [&](int j0, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
+            constexpr bool GEN = decltype(general)::value;
+            float sc[NI];
+            bool valid[NI];
+            float mx = m;
+#pragma unroll
+            for (int u = 0; u < NI; ++u) {
+                const int row = j0 + RPI * u + g;
+                valid[u] = GEN ? row < Lk : true;
+                if (GEN && row == L0) {
+                    kr[u] = knew;
+                    vr[u] = vnew;
+                }
+                float sv = F::dot(q, kr[u]);
+#pragma unroll
+                for (int off = 1; off < LPR; off <<= 1) sv += __shfl_xor(sv, off);
+                sc[u] = sv * a.scale_log2;
+                if (valid[u]) mx = fmaxf(mx, sc[u]);
+            }
+            const float alpha = exp2f(m - mx);
+            l *= alpha;
+#pragma unroll
+            for (int d = 0; d < DPL; ++d) acc[d] *= alpha;
+#pragma unroll
+            for (int u = 0; u < NI; ++u) {
+                const float p = valid[u] ? exp2f(sc[u] - mx) : 0.0f;
+                l += p;
+                float v[DPL];
+                F::unpack(vr[u], v);
+#pragma unroll
+                for (int d = 0; d < DPL; ++d) acc[d] = fmaf(p, v[d], acc[d]);
+            }
+            m = mx;
+        };
+        auto interior = [&](int j0) { return j0 >= T0 && j0 + RPI * NI <= L0; };
+        const int step = S * RPI * NI;
+        Raw kr[NI], vr[NI];
+        int j0 = s0 + wv * RPI * NI;
+        if constexpr (P > 1) {
+            for (; j0 < Lk; j0 += step) {
+                if (interior(j0)) {
+                    load_chunk(j0, std::false_type{}, kr, vr);
+                    math_chunk(j0, std::false_type{}, kr, vr);
+                } else {
+                    load_chunk(j0, std::true_type{}, kr, vr);
+                    math_chunk(j0, std::true_type{}, kr, vr);
+                }
+            }
+        } else {  // one pair per workgroup (small batches): register double buffer, as the lockstep kernel
+            Raw kn[NI], vn[NI];
+            if (j0 < Lk) {
+                if (interior(j0))
+                    load_chunk(j0, std::false_type{}, kr, vr);
+                else
+                    load_chunk(j0, std::true_type{}, kr, vr);
+            }
+            for (; j0 < Lk; j0 += step) {
+                const int j1 = j0 + step;
+                if (j1 < Lk) {
+                    if (interior(j1))
+                        load_chunk(j1, std::false_type{}, kn, vn);
+                    else
+                        load_chunk(j1, std::true_type{}, kn, vn);
+                }
+                if (interior(j0))
+                    math_chunk(j0, std::false_type{}, kr, vr);
+                else
+                    math_chunk(j0, std::true_type{}, kr, vr);
+#pragma unroll
+                for (int u = 0; u < NI; ++u) {
+                    kr[u] = kn[u];
+                    vr[u] = vn[u];
+                }
+            }
+        }
+#pragma unroll
+        for (int off = LPR; off < 64; off <<= 1) {  // merge the row groups (lanes c, c + LPR, ... hold the same dims)
+            const float mo = __shfl_xor(m, off);
+            const float lo = __shfl_xor(l, off);
+            const float mn = fmaxf(m, mo);
+            const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
+            l = l * fa + lo * fo;
+#pragma unroll
+            for (int d = 0; d < DPL; ++d) {
+                const float ao = __shfl_xor(acc[d], off);
+                acc[d] = acc[d] * fa + ao * fo;
+            }
+            m = mn;
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int d = 0; d < DPL; ++d) s_acc[t][c * DPL + d] = acc[d];
+            if (c == 0) {
+                s_m[t] = m;
+                s_l[t] = l;
+            }
+        }
+    }
+    __syncthreads();
+    if (wave >= P) return;
+    const int st = s_info[wave][5];
+    const int pair = s_info[wave][0];
+    if (st == 0) return;  // no pair, or skipped: the output row keeps its old (finite) values
+    const int b = pair / a.H, h = pair - b * a.H;
+    _Float16* orow = a.out + (int64_t)b * a.out_stride + h * ATT_D;
+    if (st == 2) {
+        orow[lane] = (_Float16)__builtin_nanf("");
+        return;
+    }
+    if (lane >= LPR) return;
+    const int S = s_info[wave][3], w0 = s_info[wave][4];
+    float mt = s_m[w0];
+    for (int w = 1; w < S; ++w) mt = fmaxf(mt, s_m[w0 + w]);
+    float l = 0.0f;
+    float acc[DPL];
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) acc[d] = 0.0f;
+    for (int w = 0; w < S; ++w) {
+        const float f = exp2f(s_m[w0 + w] - mt);
+        l += s_l[w0 + w] * f;
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) acc[d] += s_acc[w0 + w][lane * DPL + d] * f;
+    }
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int h8 = 0; h8 < DPL / 8; ++h8) {
+        f16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float tv = acc[h8 * 8 + i] * inv;
+            asm volatile("" : "+v"(tv));
+            o[i] = (_Float16)tv;
+        }
+        *(f16x8*)(orow + lane * DPL + h8 * 8) = o;
+    }
+}
+
 // fp16 -> fp8 (e4m3fn) with the same saturating round-to-nearest-even conversion as the kernel's KV append
 __global__ void quantize_fp8_kernel(const _Float16* __restrict__ src, uint32_t* __restrict__ dst, int64_t n4) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -661,6 +954,62 @@ extern "C" int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, voi
                                             d_L0 ? 0 : L0, d_L0, cap, window, d_out, out_stride, scale, hip_stream,
                                             d_done, done_stride, d_stop);
     return NS_ERR_CONFIG;
+}
+
+template <class F>
+static int paged_attention(nsg::PagedArgs a, void* hip_stream) {
+    const hipStream_t st = (hipStream_t)hip_stream;
+    const int pairs = a.B * a.H;
+    if (pairs <= NSG_ATT_SMALL_PAIRS)
+        hipLaunchKernelGGL((nsg::paged_attn_kernel<F, 1>), dim3(pairs), dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((nsg::paged_attn_kernel<F, 8>), dim3(a.H * ((a.B + 7) / 8)), dim3(512), 0, st, a);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_decode_attention_paged(const void* d_qkv, int64_t qkv_stride, const uint64_t* d_page_table,
+                                         int64_t table_stride, int max_chunks, int layer, const void* d_k_prefix,
+                                         const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D,
+                                         const int32_t* d_lens, int window, int kv_format, const uint32_t* d_done,
+                                         int64_t done_stride, const int32_t* d_stop, void* d_out, int64_t out_stride,
+                                         float scale, void* hip_stream) {
+    if (!d_qkv || !d_page_table || !d_lens || !d_out || B <= 0 || H <= 0 || T0 < 0 || layer < 0 || window < 0)
+        return NS_ERR_CONFIG;
+    if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
+    if (kv_format != NS_KV_FP16 && kv_format != NS_KV_FP8) return NS_ERR_CONFIG;
+    if (max_chunks < 1 || table_stride < max_chunks || (d_done && done_stride < 1)) return NS_ERR_CONFIG;
+    const int64_t esz = kv_format == NS_KV_FP8 ? 1 : 2;
+    if (T0 > 0 && (!d_k_prefix || !d_v_prefix || prefix_h_stride < (int64_t)T0 * D || ((prefix_h_stride * esz) & 15)))
+        return NS_ERR_CONFIG;
+    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_out | (uintptr_t)d_page_table |
+                            (uintptr_t)(T0 > 0 ? d_k_prefix : d_qkv) | (uintptr_t)(T0 > 0 ? d_v_prefix : d_qkv);
+    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || ((uintptr_t)d_lens & 3u)) return NS_ERR_CONFIG;
+    if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
+    if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
+    nsg::PagedArgs a;
+    a.qkv = (const _Float16*)d_qkv;
+    a.qkv_stride = qkv_stride;
+    a.table = d_page_table;
+    a.tstride = table_stride;
+    a.max_chunks = max_chunks;
+    a.v_off = (int64_t)H * 32 * D;
+    a.layer_off = (int64_t)layer * 2 * a.v_off;
+    a.kp = T0 > 0 ? d_k_prefix : d_qkv;
+    a.vp = T0 > 0 ? d_v_prefix : d_qkv;
+    a.ph = prefix_h_stride;
+    a.T0 = T0;
+    a.B = B;
+    a.H = H;
+    a.lens = d_lens;
+    a.window = window;
+    a.done = d_done;
+    a.done_stride = done_stride;
+    a.stop = d_stop;
+    a.out = (_Float16*)d_out;
+    a.out_stride = out_stride;
+    a.scale_log2 = scale * 1.4426950408889634f;
+    return kv_format == NS_KV_FP8 ? paged_attention<nsg::FmtF8>(a, hip_stream)
+                                  : paged_attention<nsg::FmtF16>(a, hip_stream);
 }
 
 extern "C" int ns_quantize_fp8(const void* d_src, void* d_dst, int64_t n, void* hip_stream) {

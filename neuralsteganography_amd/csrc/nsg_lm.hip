@@ -1035,11 +1035,12 @@ __device__ __forceinline__ void ln_row(float (&x)[LN_MAXV][4], int NV4, int C, c
 __global__ __launch_bounds__(256) void layernorm_kernel(const f16* __restrict__ X, int64_t ldx,
                                                         const f16* __restrict__ w, const f16* __restrict__ b,
                                                         f16* __restrict__ Y, int64_t ldy, int M, int C, float eps,
-                                                        int32_t* __restrict__ counter) {
+                                                        int32_t* __restrict__ counter, int32_t* __restrict__ row_counter) {
     if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     const int lane = threadIdx.x & 63, NV4 = C >> 2;
+    if (row_counter && lane == 0) row_counter[row] += 1;  // per-stream cache lengths (paged decode step)
     const f16* xr = X + (int64_t)row * ldx;
     float x[LN_MAXV][4];
 #pragma unroll
@@ -1059,10 +1060,12 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
                                                        const int32_t* __restrict__ dL, f16* __restrict__ H,
                                                        int64_t ldh, const f16* __restrict__ w,
                                                        const f16* __restrict__ b, f16* __restrict__ A, int64_t lda,
-                                                       int M, int C, float eps, int seq_T) {
+                                                       int M, int C, float eps, int seq_T,
+                                                       const int32_t* __restrict__ rowL) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     if (dL) L = *dL;
+    if (rowL) L = rowL[row];  // per-stream cache lengths (paged decode step, slot refill)
     // decode step: pos = L mod n_positions (code_base/arithmetic.py:44-48, L >= 0); whole sequences (seq_T > 0):
     // row b*T + t is position t (the first call's default positions)
     const int pos = seq_T > 0 ? (row % seq_T) % n_positions : L % n_positions;
@@ -1389,7 +1392,7 @@ extern "C" int ns_lm_layernorm_count(const void* d_x, int64_t ldx, const void* d
     const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_w | (uintptr_t)d_b | (uintptr_t)d_y;
     if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C || ((uintptr_t)d_counter & 3u)) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, (const f16*)d_x,
-                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps, d_counter);
+                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps, d_counter, nullptr);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
@@ -1452,7 +1455,7 @@ extern "C" int ns_lm_embed_ln(const int32_t* d_tokens, const void* d_wte, const 
     if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
                        (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, L, d_L, (f16*)d_h, ldh, (const f16*)d_w,
-                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps, 0);
+                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps, 0, nullptr);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }
 
@@ -1468,6 +1471,33 @@ extern "C" int ns_lm_embed_seq_ln(const int32_t* d_tokens, const void* d_wte, co
     if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C) return NS_ERR_CONFIG;
     hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
                        (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, 0, nullptr, (f16*)d_h, ldh,
-                       (const f16*)d_w, (const f16*)d_b, (f16*)d_a, lda, M, C, eps, T);
+                       (const f16*)d_w, (const f16*)d_b, (f16*)d_a, lda, M, C, eps, T, nullptr);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_embed_ln_rows(const int32_t* d_tokens, const void* d_wte, const void* d_wpe, int V, int n_positions,
+                                   const int32_t* d_lens, void* d_h, int64_t ldh, const void* d_w, const void* d_b,
+                                   void* d_a, int64_t lda, int M, int C, float eps, void* hip_stream) {
+    if (!d_tokens || !d_wte || !d_wpe || !d_lens || !d_h || !d_w || !d_b || !d_a || M <= 0 || C <= 0 || V <= 0 ||
+        n_positions <= 0)
+        return NS_ERR_CONFIG;
+    if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
+    const uintptr_t al = (uintptr_t)d_wte | (uintptr_t)d_wpe | (uintptr_t)d_h | (uintptr_t)d_w | (uintptr_t)d_b |
+                         (uintptr_t)d_a;
+    if ((al & 7u) || (ldh & 3) || (lda & 3) || ldh < C || lda < C || ((uintptr_t)d_lens & 3u)) return NS_ERR_CONFIG;
+    hipLaunchKernelGGL(embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, d_tokens,
+                       (const f16*)d_wte, (const f16*)d_wpe, V, n_positions, 0, nullptr, (f16*)d_h, ldh, (const f16*)d_w,
+                       (const f16*)d_b, (f16*)d_a, lda, M, C, eps, 0, d_lens);
+    return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
+}
+
+extern "C" int ns_lm_layernorm_rows(const void* d_x, int64_t ldx, const void* d_w, const void* d_b, void* d_y,
+                                    int64_t ldy, int M, int C, float eps, int32_t* d_lens, void* hip_stream) {
+    if (!d_x || !d_w || !d_b || !d_y || !d_lens || M <= 0 || C <= 0) return NS_ERR_CONFIG;
+    if (C % 4 || C > 256 * LN_MAXV) return NS_ERR_UNSUPPORTED;
+    const uintptr_t al = (uintptr_t)d_x | (uintptr_t)d_w | (uintptr_t)d_b | (uintptr_t)d_y;
+    if ((al & 7u) || (ldx & 3) || (ldy & 3) || ldx < C || ldy < C || ((uintptr_t)d_lens & 3u)) return NS_ERR_CONFIG;
+    hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)hip_stream, (const f16*)d_x,
+                       ldx, (const f16*)d_w, (const f16*)d_b, (f16*)d_y, ldy, M, C, eps, nullptr, d_lens);
     return hipGetLastError() == hipSuccess ? NS_OK : NS_ERR_HIP;
 }

@@ -52,5 +52,11 @@ class QualityGateError(NeuralStegoError):
         return "quality gate rejected the generated cover: " + "; ".join(self.reasons)
 
 
+class KVCapacityError(NeuralStegoError, RuntimeError):
+    """The paged KV cache cannot give a stream its next page: the device has no memory left for it (a library
+    error, never PyTorch's out-of-memory).  The reference keeps one unbounded cache per message
+    (``code_base/arithmetic.py:96-122``) and has no such limit short of the machine's memory."""
+
+
 __all__ = ["NeuralStegoError", "ConfigurationError", "FramingError", "PacketECCError", "PacketCRCError",
-           "MissingChunksError", "QualityGateError"]
+           "MissingChunksError", "QualityGateError", "KVCapacityError"]

@@ -155,6 +155,8 @@ class HipArithmeticLM:
 
     decodes_without_state = True  # the interval coder needs no per-token history (unlike the rank coder)
     skip_done = True  # finished streams skip their attention (encode: done flag, decode: stop position; A/B, tests)
+    slot_compaction = True  # native slot loops: compact the live slots once the queue is drained (off: tests that
+                            # read per-step logits by row)
 
     def __init__(self, model, tokenizer=None, *, device: Optional[str] = None, logits_dtype: str = "f32",
                  compute_dtype=None, banned: Optional[Sequence[int]] = None, max_batch: int = 4096,
@@ -297,8 +299,15 @@ class HipArithmeticLM:
     def encode_batch(self, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                      quality: Mapping[str, object], check_every: int = 16,
                      stall_steps: int = 4096, return_stats: bool = False, stop_text: Optional[str] = None,
-                     graphs: Optional[bool] = None):
-        """Encode B independent bit lists in lockstep (one GPT-2 forward + one coder launch per token).
+                     graphs: Optional[bool] = None, slots: Optional[int] = None):
+        """Encode independent bit lists (one GPT-2 forward + one coder launch per token for every live stream).
+
+        On the native GPU model (the product path) the messages run through ``slots`` slots (default
+        ``min(len(bit_lists), max_batch)``, :class:`~neuralsteganography_amd.lm.slots.SlotEncoder`): a finished
+        message's slot takes the next queued one, KV pages follow the live tokens (``lm/kvpages.py``), the youngest
+        messages are re-queued when the device is full, and the live slots are compacted once the queue is drained.
+        A message's tokens do not depend on its slot or neighbours (batch-invariant decode step).  Other LMs (the
+        PyTorch fp32 forward, synthetic rows) run the lockstep loop below.
 
         With ``graphs`` (default; needs the native fp16 step) the per-token step is captured once as a hipGraph
         and replayed, which removes the per-launch host cost (it dominates at small batch, and at B = 4096 it
@@ -314,16 +323,34 @@ class HipArithmeticLM:
         if B == 0:
             return []
         params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
-        ctx = self._coder(params, B)
         finish = bool(dict(quality or {}).get("finish_sent", False))
-        if finish:
-            ctx.set_sentence_end(self.sentence_end_table())
         max_bits = max(len(b) for b in bit_lists)
         budget = 2 * max_bits + 64            # initial KV/history capacity (grows on demand)
         hard_cap = 64 * max_bits + 4096       # a stream fixing < 1/64 bit per token is reported, not looped
-        logits = self.lm.prefill(context, B, budget)
         if graphs is None:
             graphs = True
+        if getattr(self.lm, "native", False):
+            from .slots import SlotEncoder
+
+            S = max(1, min(B, int(slots) if slots else self.max_batch))
+            ctx = self._coder(params, S)
+            if finish:
+                ctx.set_sentence_end(self.sentence_end_table())
+            enc = SlotEncoder(self, ctx, bit_lists, context, slots=S, finish=finish, stop_text=stop_text,
+                              stats=return_stats, check_every=check_every, stall_steps=stall_steps, hard_cap=hard_cap,
+                              use_graph=bool(graphs), compact=self.slot_compaction)
+            toks, st = enc.run()
+            self.last_schedule = {"slots": S, "evictions": enc.evictions, "compactions": enc.compactions,
+                                  "max_live": enc.max_live, "kv_pages_peak": enc.kv_peak}
+            for b in bit_lists:
+                sc = _bits_count_state(len(b))
+                self._encode_states.append(sc)
+                self._decode_states.append(dict(sc))
+            return (toks, st) if return_stats else toks
+        ctx = self._coder(params, B)
+        if finish:
+            ctx.set_sentence_end(self.sentence_end_table())
+        logits = self.lm.prefill(context, B, budget)
         use_graph = graphs and getattr(self.lm, "hip_attention", False) and hasattr(self.lm, "begin_static")
         # token history: starts at the KV budget and grows at the host checks (a captured graph holds the
         # buffer's address, so it is re-captured after a growth; the 64x hard cap up front would be 8.6 GB at
@@ -404,9 +431,12 @@ class HipArithmeticLM:
         return sess.tokens()
 
     def decode_batch(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
-                     quality: Mapping[str, object], graphs: Optional[bool] = None) -> List[List[int]]:
-        """Decode B token lists (ragged) in lockstep; returns every emitted bit (callers truncate).  With
-        ``graphs`` the per-token step (coder + GPT-2 decode) is a replayed hipGraph, as in :meth:`encode_batch`."""
+                     quality: Mapping[str, object], graphs: Optional[bool] = None,
+                     slots: Optional[int] = None) -> List[List[int]]:
+        """Decode token lists (ragged); returns every emitted bit (callers truncate).  On the native GPU model the
+        lists run through ``slots`` slots (:class:`~neuralsteganography_amd.lm.slots.SlotDecoder`, longest first,
+        a message's pages mapped when it is admitted); with ``graphs`` the per-token step (coder + GPT-2 decode) is a
+        replayed hipGraph, as in :meth:`encode_batch`."""
         import torch
 
         from ..codec.errors import DecodeDivergenceError
@@ -418,11 +448,18 @@ class HipArithmeticLM:
             if any((int(t) < 0 or int(t) >= self.vocab) for t in tl):
                 raise DecodeDivergenceError(f"received token id outside [0, {self.vocab})")
         params = coder_params_from_quality(quality, self.vocab, self.logits_dtype, self.banned)
+        if graphs is None:
+            graphs = True
+        if getattr(self.lm, "native", False):  # the product path: slots, pages mapped at admission (lm/slots.py)
+            from .slots import SlotDecoder
+
+            S = max(1, min(B, int(slots) if slots else self.max_batch))
+            dec = SlotDecoder(self, self._coder(params, S), token_lists, context, slots=S, use_graph=bool(graphs),
+                              compact=self.slot_compaction)
+            return dec.run()
         ctx = self._coder(params, B)
         sess = DecodeSession(ctx, token_lists)
         logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)
-        if graphs is None:
-            graphs = True
         native = getattr(self.lm, "native", False) and self.skip_done
         if native:
             # the forward after token t feeds token t + 1's logits: a stream of n tokens needs none once the cache

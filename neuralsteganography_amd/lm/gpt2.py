@@ -29,6 +29,7 @@ import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -56,7 +57,7 @@ class BatchedGPT2:
         cfg = hf_model.config
         self.shape = GPT2Shape(cfg.n_layer, cfg.n_head, cfg.n_embd, cfg.vocab_size, cfg.n_positions,
                                cfg.layer_norm_epsilon)
-        self.device = torch.device(device) if device is not None else next(hf_model.parameters()).device
+        self.device = _normalise_device(torch.device(device) if device is not None else next(hf_model.parameters()).device)
         if compute_dtype is None:
             compute_dtype = torch.float16 if self.device.type == "cuda" else torch.float32
         self.dtype = compute_dtype
@@ -116,8 +117,12 @@ class BatchedGPT2:
             raise ValueError("an fp8 KV cache needs the native fp16 decode step on the GPU")
         self.kv_dtype = kv_dtype
         self.kv_torch_dtype = torch.uint8 if kv_dtype == "fp8" else self.dtype
-        self.d_L = None
         self._static_logits = None
+        # native path: the paged KV cache (lm/kvpages.py) -- a pool of 32-position pages kept across calls, and the
+        # current call's page table + per-stream lengths
+        self.pool = None
+        self.kv = None
+        self.first_logits = None  # [1, ld] logits of the shared context (a refilled slot's first coder step)
         # optional per-stream done flags read by the decode attention (int32 tensor view [B], bit 0 = finished, e.g.
         # the coder state's flags word): finished streams skip their cache reads; their logits are never used again
         self.done_flags = None
@@ -226,15 +231,19 @@ class BatchedGPT2:
             self.kp = self.vp = None
 
     def grow(self, extra: int) -> None:
-        """Enlarge the KV cache by ``extra`` positions (copying the filled part); low-entropy streams can
-        need more tokens than the initial budget."""
-        s = self.shape
+        """Enlarge the dense KV cache of the PyTorch path (fp32 / CPU, the forward's reference configuration) by
+        ``extra`` positions, copying the filled part.  The copy holds the old and the new cache at once, so the
+        WHOLE new cache must fit beside the old one (the native path pages instead: no copy)."""
+        from ..exceptions import KVCapacityError
+
         new_len = self.max_len + int(extra)
-        if self.device.type == "cuda":  # the copy holds old and new caches at once
+        if self.device.type == "cuda":
             free, _ = torch.cuda.mem_get_info(self.device)
-            new_len = min(new_len, self.max_len + int(free * 0.9) // (2 * self.kv_bytes_per_position(self.B)))
+            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+            fit = (int(free * 0.9) - self.headroom_bytes(self.B)) // self.kv_bytes_per_position(self.B) + self.T0
+            new_len = min(new_len, fit)
             if new_len <= self.L:
-                raise RuntimeError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
+                raise KVCapacityError(f"KV cache full at {self.L} positions for B={self.B}: no device memory to grow")
         T0, n = self.T0, self.L - self.T0  # stream rows filled so far
         plain = self.k_cache.dim() == 5
         shp = self._cache_shape(self.B, new_len - T0, plain)
@@ -320,16 +329,15 @@ class BatchedGPT2:
                 kp[i, 0] = qkv[:, C:2 * C].view(T, H, D).transpose(0, 1)
                 vp[i, 0] = qkv[:, 2 * C:].view(T, H, D).transpose(0, 1)
 
-            self.k_cache = self.v_cache = None
+            self.kv = None
             hs = self._seq_native(ids, kv_hook=keep_kv)
             lg = self._head_native(hs[T - 1:T])
             if self.kv_dtype == "fp8":  # the context rows get the same conversion as the decode-time appends
                 kp, vp = self._quantize_fp8(kp), self._quantize_fp8(vp)
-            # the one-stream prefill cache survives as kp/vp: it is not free memory for the stream cache
-            self._allocate_fitted(B, T, max_new, T0=T)
             self.kp, self.vp = kp, vp
-            self.L = T
-            return lg.expand(B, -1).contiguous()
+            self.first_logits = lg
+            self.begin_slots(B, T, max_new)
+            return lg.repeat(B, 1)  # always a copy: slot refills write first_logits into these rows
         else:
             pos = torch.arange(T, device=self.device) % self.shape.n_positions
             h = self.wte[ids] + self.wpe[pos][None]
@@ -471,16 +479,74 @@ class BatchedGPT2:
         out = out if out.dtype == self.logits_dtype else out.to(self.logits_dtype)
         return out.view(B, T, self.ld)
 
-    def _decode_native(self, tokens: torch.Tensor, out: torch.Tensor, dev_len: bool) -> torch.Tensor:
-        """One decode step on the batch-invariant HIP kernels: embed + ln_1, then per layer c_attn GEMM, fused
-        KV-append attention, c_proj GEMM with the residual add in its epilogue, ln_2, c_fc GEMM with gelu_new in
-        its epilogue, c_proj GEMM + residual; ln_f and the head GEMM straight into ``out`` ([B, ld] logits).
-        ``dev_len``: the position / cache length come from ``self.d_L`` (graph replays)."""
+    # ------------------------------------------------------------------ paged KV (native path)
+    def _pool_budget(self) -> int:
+        """Device bytes the page pool may still take: free memory (with what PyTorch's allocator holds unused) less
+        a 5 % reserve and :meth:`headroom_bytes` for what is allocated beside the cache."""
+        free, total = torch.cuda.mem_get_info(self.device)
+        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        return int(free - 0.05 * total) - self.headroom_bytes(max(self.B, 1))
+
+    def page_pool(self):
+        from .kvpages import KVPagePool
+
+        if self.pool is None:
+            s = self.shape
+            self.pool = KVPagePool(s.n_layer, s.n_head, s.n_embd // s.n_head, self.kv_torch_dtype, self.device,
+                                   budget_bytes=self._pool_budget)
+        return self.pool
+
+    def begin_slots(self, B: int, T0: int, max_new: int = 32) -> None:
+        """A new call over ``B`` stream slots, every one at the shared context (cache length ``T0``): a fresh page
+        table (every page of the pool free again), no page assigned yet."""
+        from .kvpages import PAGE_ROWS, PagedKV
+
+        pool = self.page_pool()
+        self.kv = None
+        pool.reset()
+        self.kv = PagedKV(pool, B, T0, (max(1, int(max_new)) + PAGE_ROWS - 1) // PAGE_ROWS + 1)
+        self.B, self.L, self.T0 = int(B), int(T0), int(T0)
+        self._nb = None
+
+    def warm_pool(self, pages: int = None, B: int = 1) -> int:
+        """Grow the page pool to ``pages`` pages (default: as many as the device budget allows at batch ``B``) and
+        write every new page once, so a timed call finds its pages mapped and warm (a first pass over freshly
+        allocated device memory measured up to 12 % slower per step).  Returns the pool's size in pages."""
+        pool = self.page_pool()
+        saveB, self.B = self.B, max(self.B, int(B))
+        try:
+            want = pool.total + pool.growable_pages() if pages is None else int(pages)
+            if want > pool.total:
+                pool.add_segment(min(want - pool.total, pool.growable_pages()))
+            for seg in pool.segments:
+                seg.zero_()
+        finally:
+            self.B = saveB
+        return pool.total
+
+    def release_cache(self) -> None:
+        """Drop the paged cache, its pool and the shared context's K/V (device memory back to PyTorch)."""
+        self.kv = None
+        if self.pool is not None:
+            self.pool.release_memory()
+        self.pool = None
+        self.kp = self.vp = None
+        self.k_cache = self.v_cache = None
+        self._nb = None
+
+    def _decode_native(self, tokens: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """One decode step of every slot on the batch-invariant HIP kernels: embed + ln_1 at each stream's own
+        position (``lens[b] % n_positions``), then per layer c_attn GEMM, the paged KV-append attention
+        (``ns_decode_attention_paged``: each stream over its own pages and length), c_proj GEMM with the residual add
+        in its epilogue, ln_2, c_fc GEMM with gelu_new in its epilogue, c_proj GEMM + residual; ln_f (advancing every
+        ``lens[b]`` by one) and the head GEMM straight into ``out`` ([B, ld] logits).  Every per-step quantity lives
+        on the device, so the same launches are captured once as a hipGraph and replayed."""
         from .. import _lib
         from ..coder import _stream_handle
 
         s = self.shape
-        B, C = self.B, s.n_embd
+        kv = self.kv
+        B, C = kv.B, s.n_embd
         H, D = s.n_head, C // s.n_head
         L = _lib.lib()
         st = _stream_handle()
@@ -489,10 +555,7 @@ class BatchedGPT2:
         tok = tokens if tokens.dtype == torch.int32 else tokens.to(torch.int32)
         if not tok.is_contiguous() or tok.shape != (B,):
             tok = tok.reshape(B).contiguous()
-        dL = self.d_L.data_ptr() if dev_len else None
-        if self.L >= self.max_len:
-            raise RuntimeError("KV cache full")  # step() grows the cache before this point
-        T0 = self.T0
+        T0 = kv.T0
         eps = float(s.eps)
 
         def ok(rc, what):
@@ -504,20 +567,23 @@ class BatchedGPT2:
                             bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), B, N, K, epi,
                             st), "ns_lm_gemm")
 
-        strides = [self._cache_strides(i) for i in range(s.n_layer)]
         df = self.done_flags
-        if df is not None and (df.dtype != torch.int32 or df.shape != (B,) or df.device != self.device):
+        if df is not None and (df.dtype != torch.int32 or df.shape != (B,) or not _same_device(df.device, self.device)):
             raise ValueError(f"done_flags must be an int32 [{B}] view on {self.device}")
         done_ptr, done_stride = (df.data_ptr(), df.stride(0)) if df is not None else (None, 0)
         sl = self.stop_len
         if sl is not None and (sl.dtype != torch.int32 or sl.shape != (B,) or not sl.is_contiguous()
-                               or sl.device != self.device):
+                               or not _same_device(sl.device, self.device)):
             raise ValueError(f"stop_len must be a contiguous int32 [{B}] tensor on {self.device}")
         stop_ptr = sl.data_ptr() if sl is not None else None
+        if out.shape != (B, self.ld) or out.stride(1) != 1:
+            raise ValueError(f"logits buffer must be [{B}, {self.ld}]")
+        lens = kv.lens.data_ptr()
         lw0 = self.layers[0]
-        ok(L.ns_lm_embed_ln(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
-                            self.L, dL, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
-                            a.data_ptr(), C, B, C, eps, st), "ns_lm_embed_ln")
+        ok(L.ns_lm_embed_ln_rows(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
+                                 lens, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
+                                 a.data_ptr(), C, B, C, eps, st), "ns_lm_embed_ln_rows")
+
         def ln_gemm(ln_w, ln_b, wt, bias, y, epi, N):  # ln(h) -> GEMM, one launch at small B (same bits)
             ok(L.ns_lm_ln_gemm(h.data_ptr(), C, ln_w.data_ptr(), ln_b.data_ptr(), eps, wt.data_ptr(), wt.stride(0),
                                bias.data_ptr(), y.data_ptr(), y.stride(0), B, N, C, epi, a.data_ptr(), C, st),
@@ -528,72 +594,92 @@ class BatchedGPT2:
                 ln_gemm(lw["ln1_w"], lw["ln1_b"], lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C)
             else:  # ln_1 of layer 0 comes with the embedding
                 gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
-            kc, vc = self.k_cache[i], self.v_cache[i]
-            sb, sh, sz = strides[i]
             kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
             vp = self.vp[i, 0] if T0 else None
-            rc = self._attn(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), sb, sh, sz,
-                            kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
-                            kp.stride(0) if T0 else 0, T0, B, H, D, self.L, dL, self.max_len, self.window,
-                            self._kv_format, done_ptr, done_stride, stop_ptr, o.data_ptr(), o.stride(0),
-                            1.0 / math.sqrt(D), st)
-            ok(rc, "ns_decode_attention_prefix")
+            rc = L.ns_decode_attention_paged(qkv.data_ptr(), qkv.stride(0), kv.table.data_ptr(), kv.table.stride(0),
+                                             kv.width, i, kp.data_ptr() if T0 else None,
+                                             vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D,
+                                             lens, self.window, self._kv_format, done_ptr, done_stride, stop_ptr,
+                                             o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
+            ok(rc, "ns_decode_attention_paged")
             gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
             ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)
             gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
-        # ln_f; with a device-side length it also advances d_L for the next step (no launch of its own)
-        ok(L.ns_lm_layernorm_count(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B,
-                                   C, eps, dL, st), "ns_lm_layernorm_count")
+        # ln_f also advances every stream's cache length (no launch of its own)
+        ok(L.ns_lm_layernorm_rows(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B,
+                                  C, eps, lens, st), "ns_lm_layernorm_rows")
         epi = _lib.NS_LM_EPI_STORE_F32 if out.dtype == torch.float32 else _lib.NS_LM_EPI_STORE
-        if out.shape != (B, self.ld) or out.stride(1) != 1:
-            raise ValueError(f"logits buffer must be [{B}, {self.ld}]")
         gemm(a, self.head_t, None, out, epi, self.ld, C)
         return out
 
     # ------------------------------------------------------------------ graph-capturable decode step
     def begin_static(self, logits_out: torch.Tensor) -> None:
-        """Prepare :meth:`step_static`: the cache length moves to a device int32 (``d_L``) and the logits go to
-        the fixed buffer ``logits_out`` ([B, ld]), so the same captured hipGraph replays every decode step.
-        Needs the HIP attention path (fp16 on the GPU)."""
+        """Prepare :meth:`step_static`: the logits go to the fixed buffer ``logits_out`` ([B, ld]) -- positions
+        and cache lengths already live on the device -- so the same captured hipGraph replays every decode step.
+        Needs the native HIP step (fp16 on the GPU)."""
         if not self.native:
             raise RuntimeError("graph-captured decode steps need the native HIP step (fp16 on the GPU)")
-        if logits_out.shape != (self.B, self.ld) or logits_out.dtype != self.logits_dtype:
-            raise ValueError(f"static logits must be [{self.B}, {self.ld}] {self.logits_dtype}")
-        self.d_L = torch.full((1,), self.L, dtype=torch.int32, device=self.device)
+        if logits_out.shape != (self.kv.B, self.ld) or logits_out.dtype != self.logits_dtype:
+            raise ValueError(f"static logits must be [{self.kv.B}, {self.ld}] {self.logits_dtype}")
         self._static_logits = logits_out
 
     def static_capacity_left(self) -> int:
-        """Decode steps that still fit the preallocated cache (graph replays cannot grow it)."""
-        return self.max_len - self.L
+        """Decode steps every slot can take within the pages it holds (graph replays cannot map pages)."""
+        return self.kv.steps_reserved(np.arange(self.kv.B))
+
+    def reserve(self, steps: int) -> bool:
+        """Lockstep callers: map the pages every slot needs for the next ``steps`` decode steps (False: the device
+        has no memory for them)."""
+        return self.kv.ensure(np.arange(self.kv.B), self.L + int(steps)).size == 0
+
+    def advance(self, n: int = 1) -> None:
+        """The host side of ``n`` executed decode steps (the device advanced ``lens`` itself)."""
+        self.L += int(n)
+        self.kv.advance(n)
 
     @torch.no_grad()
     def step_static(self, tokens: torch.Tensor) -> torch.Tensor:
-        """:meth:`step` with every per-step quantity on the device: position ``d_L % n_positions``, the
-        attention's cache length read from ``d_L``, logits written into the fixed buffer, ``d_L += 1`` (by the
-        final layer norm's launch).  Issues no host synchronisation and no allocation that depends on the step, so
-        it can be captured once.  The caller advances the host-side ``L`` by one per executed step."""
-        self._decode_native(tokens, self._static_logits, dev_len=True)
+        """:meth:`step` into the fixed logits buffer, without host-side page mapping or length bookkeeping: issues no
+        host synchronisation and no allocation, so it can be captured once.  The caller maps pages ahead
+        (:meth:`reserve`, or the slot scheduler) and calls :meth:`advance` per executed step."""
+        self._decode_native(tokens, self._static_logits)
         return self._static_logits
 
     @torch.no_grad()
     def step(self, tokens: torch.Tensor) -> torch.Tensor:
         """Feed one token per stream (``[B]`` int); position = cache length mod n_positions."""
         B = self.B
-        if self.L >= self.max_len:
-            self.grow(max(64, self.max_len))
         if tokens.shape != (B,):
             raise ValueError(f"expected {B} tokens")
         if self.native:
+            if not self.reserve(1):
+                from ..exceptions import KVCapacityError
+
+                raise KVCapacityError(f"KV cache full at {self.L} positions for B={B}: no device memory for a page")
             out = torch.empty((B, self.ld), device=self.device, dtype=self.logits_dtype)
-            self._decode_native(tokens, out, dev_len=False)
-            self.L += 1
+            self._decode_native(tokens, out)
+            self.advance(1)
             return out
+        if self.L >= self.max_len:
+            self.grow(max(64, self.max_len))
         pos = self.L % self.shape.n_positions
         h = (self.wte[tokens.long()] + self.wpe[pos])[:, None, :]
         for i in range(self.shape.n_layer):
             h = self._block(i, h, 1, causal=False)
         self.L += 1
         return self._logits(h[:, -1])
+
+
+def _normalise_device(dev: torch.device) -> torch.device:
+    """``cuda`` without an index is the current device (a tensor's device always carries its index: comparing
+    ``torch.device('cuda')`` with ``cuda:0`` is False)."""
+    if dev.type == "cuda" and dev.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def _same_device(a: torch.device, b: torch.device) -> bool:
+    return a.type == b.type and (a.index or 0) == (b.index or 0)
 
 
 def random_gpt2(name: str = "gpt2", *, seed: int = 1234, **overrides):

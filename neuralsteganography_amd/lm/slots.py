@@ -1,0 +1,433 @@
+"""Slot schedulers of the native encode / decode loops (round 6): slot refill, page mapping, eviction, compaction.
+
+The reference encodes every message in its own loop with its own KV cache (``code_base/arithmetic.py:96-122``; the
+api splits a secret into independent chunks, ``src/neuralstego/api.py:736-747``).  Batched on the GPU, B messages
+share one decode step; covers differ in length (a peaked, trained-LM-like row gives far longer covers than the
+mean), so a lockstep batch spends its steps on finished streams.  Here messages queue for S SLOTS:
+
+* every slot runs one message from the shared context (cache length ``T0``, the prefill's logits as its first
+  coder step's row) to its end, with its own cache length and position ids (``lens[b] % n_positions``,
+  ``code_base/arithmetic.py:44-48``) and its own KV pages (``lm/kvpages.py``);
+* every ``check_every`` steps the host reads the coder states once: finished slots hand their tokens (or bits) over
+  and take the next queued message; pages are mapped ahead for the live slots;
+* when the device runs out of pages, the youngest live messages are EVICTED (pages returned, message re-queued and
+  later re-run from its start -- the same tokens, since a stream's result does not depend on its neighbours) rather
+  than failing; a message that cannot fit alone raises :class:`KVCapacityError`;
+* when the queue is empty and at most half the slots are live, the live slots are COMPACTED into a smaller batch
+  (page tables move with their rows, no KV is copied): the GEMMs stop computing finished rows.
+
+A stream's logits are bit-identical whatever the batch it runs in (the decode step is batch-invariant, including the
+paged attention), so a message's tokens are the same alone, in lockstep, or refilled into any slot.  Between host
+checks the step (coder + GPT-2 decode) is one captured hipGraph replay; a graph is re-captured when a buffer it
+holds is replaced (a wider page table, a longer history, a compaction).
+"""
+
+from __future__ import annotations
+
+from collections import deque
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .. import _lib
+from ..coder import EncodeSession, _state_fields, _stats_rows
+from ..exceptions import KVCapacityError
+
+
+class _SlotGraph:
+    """``body()`` (one whole step into fixed buffers) run once eagerly on a side stream -- a real step, which also
+    warms every kernel up -- then captured as a hipGraph and replayed per later step."""
+
+    def __init__(self, body):
+        import torch
+
+        self.body = body
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            body()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            body()
+
+    def replay(self) -> None:
+        self.graph.replay()
+
+
+def _layout_key(*tensors) -> tuple:
+    return tuple(t.data_ptr() if t is not None else 0 for t in tensors)
+
+
+class SlotEncoder:
+    """Encode ``bit_lists`` through ``slots`` slots of ``provider.lm`` (a native :class:`BatchedGPT2`)."""
+
+    def __init__(self, provider, ctx, bit_lists: Sequence[Sequence[int]], context: Sequence[int], *, slots: int,
+                 finish: bool, stop_text: Optional[str], stats: bool, check_every: int, stall_steps: int,
+                 hard_cap: int, use_graph: bool, compact: bool = True):
+        self.p, self.lm, self.ctx = provider, provider.lm, ctx
+        self.bits = bit_lists
+        self.N = len(bit_lists)
+        self.S = max(1, min(int(slots), self.N))
+        self.context = context
+        self.finish, self.stop_text, self.stats = finish, stop_text, stats
+        self.check_every, self.stall_steps, self.hard_cap = int(check_every), int(stall_steps), int(hard_cap)
+        self.use_graph, self.allow_compact = use_graph, compact
+        self.evictions = 0
+        self.compactions = 0
+        self.max_live = 0
+        self.kv_peak = 0
+
+    # ------------------------------------------------------------------
+    def run(self):
+        import torch
+
+        from ..codec.errors import ArithmeticRangeError
+        from .arithmetic import _StopCheck
+
+        lm, S, N = self.lm, self.S, self.N
+        max_bits = max(len(b) for b in self.bits)
+        budget = 2 * max_bits + 64
+        logits = lm.prefill(self.context, S, budget)  # [S, ld]: every slot starts on the context's logits
+        first = lm.first_logits
+        T0 = lm.kv.T0
+        stride = max(1, (max_bits + 7) // 8)
+        sess = EncodeSession(self.ctx, self.bits[:S], max_tokens=budget, stats=self.stats, payload_stride=stride)
+        stop = _StopCheck(self.p, sess, self.stop_text) if self.stop_text is not None else None
+        slot_msg = np.arange(S, dtype=np.int64)  # message per slot, -1 = empty
+        queue = deque(range(S, N))
+        tokens: List[Optional[List[int]]] = [None] * N
+        stats_out: List[Optional[dict]] = [None] * N
+        last_pos = np.zeros(S, dtype=np.int64)
+        last_move = np.zeros(S, dtype=np.int64)
+        t = 0
+        graph, gkey = None, None
+        admit_blocked = False
+
+        def body():
+            tok = sess.step(logits, finish_sent=self.finish)
+            if stop is not None:
+                stop.flag(tok)
+            lm.step_static(tok)
+
+        skip = getattr(self.p, "skip_done", True)  # finished streams skip their attention (A/B switch)
+
+        def done_view():
+            return sess.state.view(torch.int32)[:, 7] if skip else None
+
+        lm.begin_static(logits)
+        lm.done_flags = done_view()
+        try:
+            while True:
+                if stop is not None and t > 0:
+                    stop.check()
+                if t % self.check_every == 0:
+                    f = sess.fields()
+                    live = slot_msg >= 0
+                    flags = f["flags"]
+                    # ---- harvest finished slots
+                    fin = np.nonzero(live & ((flags & _lib.NS_ST_DONE) != 0))[0]
+                    if fin.size:
+                        bad = fin[(flags[fin] & _lib.NS_ST_ERR_RANGE) != 0]
+                        if bad.size:
+                            raise ArithmeticRangeError(
+                                f"streams {slot_msg[bad].tolist()[:8]} found no CDF bucket for the payload index")
+                        nt = f["ntokens"][fin]
+                        if int(nt.max(initial=0)) > sess.hist.shape[1]:
+                            raise RuntimeError("token history overflow")
+                        rows = sess.hist[torch.as_tensor(fin, device=sess.hist.device), : max(1, int(nt.max()))]
+                        host = rows.cpu().numpy()
+                        acc = sess.stats_acc[torch.as_tensor(fin, device=sess.hist.device)].cpu().numpy() \
+                            if self.stats else None
+                        for j, s in enumerate(fin.tolist()):
+                            m = int(slot_msg[s])
+                            tokens[m] = host[j, : int(nt[j])].tolist()
+                            if self.stats:
+                                stats_out[m] = _stats_rows(acc[j:j + 1], f["bit_pos"][s:s + 1])[0]
+                        lm.kv.release(fin)
+                        slot_msg[fin] = -1
+                        admit_blocked = False
+                        live = slot_msg >= 0
+                    # ---- stalls (the reference loops forever on a stream that fixes no bit)
+                    pos = f["bit_pos"]
+                    moved = live & (pos != last_pos)
+                    last_pos[moved], last_move[moved] = pos[moved], t
+                    stuck = np.nonzero(live & (((t - last_move) >= self.stall_steps) |
+                                               (f["ntokens"] >= self.hard_cap)))[0]
+                    if stuck.size:
+                        ids = slot_msg[stuck].tolist()[:8]
+                        if all(pos[s] >= len(self.bits[slot_msg[s]]) for s in stuck):
+                            raise ArithmeticRangeError(
+                                f"finish_sent: streams {ids} produced no sentence-ending token in "
+                                f"{self.stall_steps} tokens (the reference would keep generating forever)")
+                        raise ArithmeticRangeError(
+                            f"streams {ids} fixed no payload bit for {self.stall_steps} tokens: the interval "
+                            "straddles the midpoint and one token takes the whole range (the reference coder "
+                            "has no underflow handling and would loop forever)")
+                    # ---- refill empty slots from the queue
+                    empty = np.nonzero(~live)[0]
+                    if queue and empty.size and not admit_blocked:
+                        room = lm.pool.free_pages + lm.pool.growable_pages() - int(live.sum()) - 1
+                        n_adm = int(min(empty.size, len(queue), max(0, room)))
+                        if n_adm:
+                            sl = empty[:n_adm]
+                            ms = [queue.popleft() for _ in range(n_adm)]
+                            self._admit(sess, logits, first, sl, ms, slot_msg, last_pos, last_move, t)
+                            live = slot_msg >= 0
+                    nlive = int(live.sum())
+                    self.max_live = max(self.max_live, nlive)
+                    if nlive == 0:
+                        if not queue:
+                            break
+                        raise KVCapacityError("no device memory for even one stream's first KV page")
+                    # ---- compaction: the queue is drained and at most half the slots are live
+                    if self.allow_compact and not queue and nlive <= sess.B // 2 and sess.B > 1:
+                        keep = np.nonzero(live)[0]
+                        sess, logits, slot_msg, last_pos, last_move = self._compact(
+                            sess, logits, keep, slot_msg, last_pos, last_move, stop)
+                        if stop is not None:
+                            stop.sess = sess
+                            stop.hit = torch.zeros(sess.B, dtype=torch.bool, device=sess.state.device)
+                        live = slot_msg >= 0
+                        self.compactions += 1
+                    # ---- pages for the next check_every + 1 steps; evict the youngest when the device is full
+                    self._map_pages(sess, slot_msg, queue, live, T0)
+                    if (slot_msg >= 0).sum() < nlive:
+                        admit_blocked = True
+                    # ---- token history for the next steps
+                    if int(f["ntokens"].max(initial=0)) + self.check_every + 1 > sess.hist.shape[1]:
+                        sess.ensure_history(self.check_every + 1)
+                    if stop is not None:
+                        stop.sess = sess
+                key = _layout_key(logits, sess.state, sess.hist, sess.payload, lm.kv.table, lm.kv.lens,
+                                  sess.stats_acc) + (lm.kv.version,)
+                if self.use_graph:
+                    if graph is None or key != gkey:
+                        graph = None
+                        lm.done_flags = done_view()
+                        lm.begin_static(logits)
+                        graph, gkey = _SlotGraph(body), key
+                    else:
+                        graph.replay()
+                else:
+                    lm.done_flags = done_view()
+                    lm.begin_static(logits)
+                    body()
+                lm.advance(1)
+                t += 1
+        finally:
+            lm.done_flags = None
+            del graph
+        self.sess = sess
+        self.kv_peak = lm.kv.peak
+        return tokens, (stats_out if self.stats else None)
+
+    # ------------------------------------------------------------------
+    def _admit(self, sess, logits, first, slots, msgs, slot_msg, last_pos, last_move, t):
+        import torch
+
+        lm = self.lm
+        sess.load_slots(slots, [self.bits[m] for m in msgs])
+        lm.kv.reset(slots)
+        idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=logits.device)
+        logits.index_copy_(0, idx, first.expand(len(slots), -1).to(logits.dtype))
+        slot_msg[slots] = msgs
+        last_pos[slots] = 0
+        last_move[slots] = t
+
+    def _map_pages(self, sess, slot_msg, queue, live, T0):
+        """Pages for every live slot's next ``check_every + 1`` positions; on a full device evict the youngest live
+        messages (fewest tokens) back to the queue's front until the others are served."""
+        lm = self.lm
+        while True:
+            sl = np.nonzero(slot_msg >= 0)[0]
+            if sl.size == 0:
+                return
+            failed = lm.kv.ensure(sl, lm.kv.lens_host[sl] + self.check_every + 1)
+            if failed.size == 0:
+                return
+            if sl.size == 1:
+                raise KVCapacityError(
+                    f"message {int(slot_msg[sl[0]])} needs more KV pages than the device holds "
+                    f"({lm.pool.total} pages of {lm.pool.page_bytes} B)")
+            nt = _state_fields(sess.state)["ntokens"]
+            victim = np.asarray([sl[np.argmin(nt[sl])]])
+            queue.appendleft(int(slot_msg[victim[0]]))
+            lm.kv.release(victim)
+            sess.park_slots(victim)
+            slot_msg[victim] = -1
+            self.evictions += 1
+
+    def _compact(self, sess, logits, keep, slot_msg, last_pos, last_move, stop):
+        import torch
+
+        lm = self.lm
+        empty = np.setdiff1d(np.arange(sess.B), keep)
+        lm.kv.release(empty)
+        lm.kv.compact(keep)
+        lm.B = lm.kv.B
+        sess.compact(keep)
+        idx = torch.as_tensor(keep, device=logits.device)
+        logits = logits.index_select(0, idx).contiguous()
+        return sess, logits, slot_msg[keep].copy(), last_pos[keep].copy(), last_move[keep].copy()
+
+
+class SlotDecoder:
+    """Decode ``token_lists`` through ``slots`` slots: every message's tokens are known, so admission maps all of a
+    message's pages up front (no eviction) and a slot's end is known on the host (no state read to find it)."""
+
+    def __init__(self, provider, ctx, token_lists: Sequence[Sequence[int]], context: Sequence[int], *, slots: int,
+                 use_graph: bool, check_every: int = 16, compact: bool = True):
+        self.p, self.lm, self.ctx = provider, provider.lm, ctx
+        self.lists = token_lists
+        self.N = len(token_lists)
+        self.S = max(1, min(int(slots), self.N))
+        self.context = context
+        self.use_graph, self.check_every, self.allow_compact = use_graph, int(check_every), compact
+        self.compactions = 0
+
+    def run(self) -> List[List[int]]:
+        import torch
+
+        from .. import _lib as L
+        from ..codec.errors import DecodeDivergenceError
+        from ..coder import _bit_rows_to_lists, _ptr, _state_tensor, _stream_handle
+
+        lm, S, N = self.lm, self.S, self.N
+        lens_all = np.asarray([len(t) for t in self.lists], dtype=np.int64)
+        Tcap = max(1, int(lens_all.max(initial=0)))
+        order = np.argsort(-lens_all, kind="stable")  # longest first: the tail is short messages
+        logits = lm.prefill(self.context, S, Tcap + 1)
+        first = lm.first_logits
+        T0 = lm.kv.T0
+        dev = logits.device
+        P = self.ctx.params.precision
+        out_stride = int((Tcap * P + P + 7) // 8 + 8)
+        st = {"tokmat": torch.zeros((S, Tcap), dtype=torch.int32, device=dev),
+              "nlen": torch.zeros(S, dtype=torch.int32, device=dev),
+              "stop": torch.zeros(S, dtype=torch.int32, device=dev),
+              "state": _state_tensor(S, dev),
+              "out_bits": torch.zeros((S, out_stride), dtype=torch.uint8, device=dev)}
+        self.ctx.check(L.lib().ns_init_state(self.ctx._h, _ptr(st["state"]), S, _stream_handle()), "ns_init_state")
+        st["state"].view(torch.int32)[:, 7] = L.NS_ST_DONE
+        slot_msg = np.full(S, -1, dtype=np.int64)
+        nlen_host = np.zeros(S, dtype=np.int64)
+        queue = deque(order.tolist())
+        out: List[Optional[List[int]]] = [None] * N
+        init_row = torch.tensor([[0, 1 << P, 0, 0]], dtype=torch.int64, device=dev)
+        p = self.ctx.params
+        graph, gkey = None, None
+        bufs = {}
+
+        def body():
+            tix = lm.kv.lens - T0
+            idx = tix.clamp(0, Tcap - 1).long().unsqueeze(1)
+            tok = torch.gather(st["tokmat"], 1, idx).squeeze(1).contiguous()
+            act = (tix < st["nlen"]).to(torch.uint8)
+            last = (tix == st["nlen"] - 1).to(torch.uint8)
+            bufs["tok"], bufs["act"], bufs["last"] = tok, act, last
+            rc = L.lib().ns_decode_step(self.ctx._h, _ptr(logits), logits.stride(0), st["state"].shape[0], _ptr(tok),
+                                        _ptr(last), _ptr(act), _ptr(st["state"]), _ptr(st["out_bits"]), out_stride,
+                                        float(p.temp), int(p.topk), self.ctx._banned, self.ctx._nbanned, None, 0,
+                                        _stream_handle())
+            self.ctx.check(rc, "ns_decode_step")
+            lm.step_static(tok)
+
+        t = 0
+        try:
+            while True:
+                if t % self.check_every == 0:
+                    live = slot_msg >= 0
+                    done = live & ((lm.kv.lens_host - T0) >= nlen_host)
+                    fin = np.nonzero(done)[0]
+                    if fin.size:
+                        f = _state_fields(st["state"])
+                        bad = fin[(f["flags"][fin] & L.NS_ST_ERR_DIVERGE) != 0]
+                        if bad.size:
+                            raise DecodeDivergenceError(
+                                f"streams {slot_msg[bad].tolist()[:8]}: received token outside the kept top-k")
+                        rows = st["out_bits"][torch.as_tensor(fin, device=dev)]
+                        got = _bit_rows_to_lists(rows, f["bit_pos"][fin])
+                        for j, s in enumerate(fin.tolist()):
+                            out[int(slot_msg[s])] = got[j]
+                        lm.kv.release(fin)
+                        slot_msg[fin] = -1
+                        nlen_host[fin] = 0
+                        fi = torch.as_tensor(fin, device=dev)
+                        st["nlen"][fi] = 0
+                        st["stop"][fi] = 0
+                        live = slot_msg >= 0
+                    empty = np.nonzero(~live)[0]
+                    adm_s, adm_m = [], []
+                    for s in empty.tolist():
+                        if not queue:
+                            break
+                        m = queue[0]
+                        n = int(lens_all[m])
+                        lm.kv.reset([s])
+                        if lm.kv.ensure([s], T0 + n).size:
+                            if not live.any() and not adm_s:
+                                raise KVCapacityError(f"message {m} ({n} tokens) needs more KV pages than the "
+                                                      "device holds")
+                            break
+                        queue.popleft()
+                        adm_s.append(s)
+                        adm_m.append(m)
+                    if adm_s:
+                        self._admit(st, logits, first, init_row, adm_s, adm_m, slot_msg, nlen_host, T0, Tcap)
+                        live = slot_msg >= 0
+                    if not live.any():
+                        break
+                    if self.allow_compact and not queue and int(live.sum()) <= st["state"].shape[0] // 2 and \
+                            st["state"].shape[0] > 1:
+                        keep = np.nonzero(live)[0]
+                        lm.kv.release(np.setdiff1d(np.arange(st["state"].shape[0]), keep))
+                        lm.kv.compact(keep)
+                        lm.B = lm.kv.B
+                        ki = torch.as_tensor(keep, device=dev)
+                        for k in st:
+                            st[k] = st[k].index_select(0, ki).contiguous()
+                        logits = logits.index_select(0, ki).contiguous()
+                        slot_msg, nlen_host = slot_msg[keep].copy(), nlen_host[keep].copy()
+                        self.compactions += 1
+                    lm.stop_len = st["stop"] if getattr(self.p, "skip_done", True) else None
+                key = _layout_key(logits, st["state"], st["tokmat"], lm.kv.table, lm.kv.lens) + (lm.kv.version,)
+                if self.use_graph:
+                    if graph is None or key != gkey:
+                        graph = None
+                        lm.begin_static(logits)
+                        graph, gkey = _SlotGraph(body), key
+                    else:
+                        graph.replay()
+                else:
+                    lm.begin_static(logits)
+                    body()
+                lm.advance(1)
+                t += 1
+        finally:
+            lm.stop_len = None
+            del graph
+        return out
+
+    def _admit(self, st, logits, first, init_row, slots, msgs, slot_msg, nlen_host, T0, Tcap):
+        import torch
+
+        dev = logits.device
+        n = len(slots)
+        mat = np.zeros((n, Tcap), dtype=np.int32)
+        nl = np.zeros(n, dtype=np.int64)
+        for i, m in enumerate(msgs):
+            tl = self.lists[m]
+            nl[i] = len(tl)
+            if len(tl):
+                mat[i, : len(tl)] = np.asarray(tl, dtype=np.int32)
+        idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=dev)
+        st["tokmat"][idx] = torch.from_numpy(mat).to(dev)
+        nlt = torch.from_numpy(nl.astype(np.int32)).to(dev)
+        st["nlen"][idx] = nlt
+        st["stop"][idx] = nlt + (T0 - 1)
+        st["state"][idx] = init_row.expand(n, 4)
+        st["out_bits"][idx] = 0
+        logits.index_copy_(0, idx, first.expand(n, -1).to(logits.dtype))
+        slot_msg[slots] = msgs
+        nlen_host[slots] = nl

@@ -255,13 +255,12 @@ def test_gpt2_fp16_decode_hip_attention_matches_sdpa_and_hf(B):
     assert (la[row, :50257].float().cpu() - ref).abs().max().item() < 3e-2
 
 
-@pytest.mark.parametrize("cap_extra,topk,n", [(None, 300, 3), (12, 300, 3), (None, 50000, 3), (None, 300, 1)])
-def test_graph_captured_encode_matches_eager(cap_extra, topk, n):
-    """encode_batch with the per-token step captured as a hipGraph (coder + GPT-2 decode, cache length on the
-    device) gives the same tokens as the eager loop, including when the preallocated cache runs out and the
-    loop continues eagerly (cap_extra: cache limited to context + 12 positions), and for the api default
-    quality (precision 16, topk 50,000), whose wide-path launches (memset, fused scan, device-wide sort,
-    list kernel) are captured too."""
+@pytest.mark.parametrize("cap_pages,topk,n", [(None, 300, 3), (3, 300, 3), (None, 50000, 3), (None, 300, 1)])
+def test_graph_captured_encode_matches_eager(cap_pages, topk, n):
+    """encode_batch with the per-token step captured as a hipGraph (coder + GPT-2 decode, cache lengths on the
+    device) gives the same tokens as the eager loop, including when the page pool is capped (cap_pages: the
+    youngest streams are re-queued, the graph re-captured), and for the api default quality (precision 16, topk
+    50,000), whose wide-path launches (memset, fused scan, device-wide sort, list kernel) are captured too."""
     from neuralsteganography_amd.lm.arithmetic import HipArithmeticLM
     from neuralsteganography_amd.lm.gpt2 import random_gpt2
 
@@ -273,8 +272,9 @@ def test_graph_captured_encode_matches_eager(cap_extra, topk, n):
     out = {}
     for graphs in (False, True):
         lm = HipArithmeticLM(m, None, logits_dtype="f16")
-        if cap_extra is not None:
-            lm.lm.fit_positions = lambda B, want, reserve=0.15: len(ctx) + cap_extra
+        if cap_pages is not None:
+            pool = lm.lm.page_pool()
+            pool.budget_bytes = lambda: (cap_pages - pool.total) * pool.page_bytes
         out[graphs] = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
         dec = lm.decode_batch(out[graphs], ctx, quality=q, graphs=graphs)
         assert all(d[: len(b)] == b for d, b in zip(dec, bits))
