@@ -92,8 +92,10 @@ int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, void* d_k_cach
 /* ns_decode_attention_ex over a PAGED cache with a cache length PER STREAM (round 6: slot refill and growth
  * without a copy).  Stream b's rows live in 32-position pages: d_page_table[b * table_stride + c] (uint64) is the
  * device address (16-byte aligned; 0 = none) of the page holding its stream rows 32c .. 32c + 31, i.e. positions
- * T0 + 32c ...; a page holds every layer, laid out [layer][K|V][H][32][D] in the kv_format's element type, so
- * `layer` selects the block at layer * 2*H*32*D elements.  d_lens[b] (int32) = positions already cached for stream b
+ * T0 + 32c ...; this layer's block of the page starts `layer_offset` elements after that address and holds
+ * [K|V][H][32][D] in the kv_format's element type (K at +0, V at +H*32*D; the pool decides where the layers of a page
+ * live: layer * 2*H*32*D for pages holding every layer back to back, layer * SEG * 2*H*32*D for segments of SEG pages
+ * stored layer-major).  d_lens[b] (int32) = positions already cached for stream b
  * (the new token is written at position d_lens[b] and attended with positions 0 .. d_lens[b]); positions < T0 come
  * from the shared prefix as in ns_decode_attention_prefix.  Only table entries 0 .. max_chunks-1 are read; a stream
  * whose new-token page is missing gets NaN output rows (the coder rejects them) and writes nothing.  d_done / d_stop
@@ -102,7 +104,7 @@ int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, void* d_k_cach
  * bits equal ns_decode_attention_ex's, whatever the batch, the other streams' lengths or where the pages live.
  * Replaces the reference's per-message cache of code_base/arithmetic.py:96-122 (each message its own loop). */
 int ns_decode_attention_paged(const void* d_qkv, int64_t qkv_stride, const uint64_t* d_page_table,
-                              int64_t table_stride, int max_chunks, int layer, const void* d_k_prefix,
+                              int64_t table_stride, int max_chunks, int64_t layer_offset, const void* d_k_prefix,
                               const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D,
                               const int32_t* d_lens, int window, int kv_format, const uint32_t* d_done,
                               int64_t done_stride, const int32_t* d_stop, void* d_out, int64_t out_stride, float scale,

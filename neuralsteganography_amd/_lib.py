@@ -142,7 +142,7 @@ def lib() -> ctypes.CDLL:
     L.ns_decode_attention_ex.argtypes = [vp, i64, vp, vp, i64, i64, i64, vp, vp, i64, ci, ci, ci, ci, ci, vp, ci, ci, ci,
                                          vp, i64, vp, vp, i64, ctypes.c_float, vp]
     L.ns_decode_attention_paged.restype = ci
-    L.ns_decode_attention_paged.argtypes = [vp, i64, vp, i64, ci, ci, vp, vp, i64, ci, ci, ci, ci, vp, ci, ci, vp, i64,
+    L.ns_decode_attention_paged.argtypes = [vp, i64, vp, i64, ci, i64, vp, vp, i64, ci, ci, ci, ci, vp, ci, ci, vp, i64,
                                             vp, vp, i64, ctypes.c_float, vp]
     L.ns_lm_embed_ln_rows.restype = ci
     L.ns_lm_embed_ln_rows.argtypes = [vp, vp, vp, ci, ci, vp, vp, i64, vp, vp, vp, i64, ci, ci, ctypes.c_float, vp]

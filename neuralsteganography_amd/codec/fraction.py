@@ -140,11 +140,24 @@ class _Device:
         while pending.any():
             table = int(self.tables[pending].min())
             grp = pending & (self.tables == table)
-            pending &= ~grp
             n = int(grp.sum())
             if self.L.ns_frac_scratch_bytes(self.ctx, n, ld, max_bits, table) > SCRATCH_BUDGET_BYTES:
-                status[grp] = NS_FRAC_ERR_CAPACITY
-                continue
+                # over the scratch budget together: launch as many as fit (a stream fails only if it
+                # cannot fit alone, never because of what else is in the batch); the rest stay pending
+                one = int(self.L.ns_frac_scratch_bytes(self.ctx, 1, ld, max_bits, table))
+                if one > SCRATCH_BUDGET_BYTES:
+                    status[grp] = NS_FRAC_ERR_CAPACITY
+                    pending &= ~grp
+                    continue
+                fit = max(1, SCRATCH_BUDGET_BYTES // one)
+                while fit > 1 and \
+                        self.L.ns_frac_scratch_bytes(self.ctx, fit, ld, max_bits, table) > SCRATCH_BUDGET_BYTES:
+                    fit -= 1
+                idx = np.nonzero(grp)[0]
+                grp = np.zeros_like(grp)
+                grp[idx[:fit]] = True
+                n = int(fit)
+            pending &= ~grp
             d_slot = torch.from_numpy(np.where(grp, np.cumsum(grp) - 1, -1).astype(np.int32)).to(self.dev)
             self.check(self.L.ns_frac_set_slots(self.ctx, d_slot.data_ptr(), n), "ns_frac_set_slots")
             try:

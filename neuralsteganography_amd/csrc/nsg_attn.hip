@@ -447,60 +447,71 @@ struct PagedArgs {
     float scale_log2;
 };
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {  // lane uniform: the value lands in SGPRs
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <class F, int P>
-__global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 : 1))) void paged_attn_kernel(
+    const PagedArgs a) {
     typedef typename F::Elem E;
     typedef typename F::Raw Raw;
     constexpr int DPL = F::DPL, LPR = F::LPR, RPI = F::RPI, NI = F::NI;
+    static_assert(RPI * NI == 32, "one iteration = one page's worth of rows");
     constexpr int NT = 8 * P;  // at most 8 splits per pair
     __shared__ float s_m[NT], s_l[NT];
     __shared__ float s_acc[NT][ATT_D];
-    __shared__ int s_info[P][6];  // pair, L0, s0, S, first task, status (0 none / skipped, 1 run, 2 poison)
-    __shared__ int s_ntask;
+    __shared__ int s_pi[8][P][4];  // per wave: pair, L0, s0 and first task of each of the workgroup's pairs
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    if (wave == 0) {  // lane j < P: pair j's length, skip flags and split; an exclusive prefix sum gives its tasks
-        int pair = -1, L0 = 0, s0 = 0, S = 0, st = 0;
-        if (lane < P) {
-            pair = att_pair<P>(blockIdx.x, lane, a.B, a.H);
-            if (pair >= 0) {
-                const int b = pair / a.H;
-                L0 = a.lens[b];
-                const bool skip = (a.done && (a.done[(int64_t)b * a.done_stride] & 1u)) || (a.stop && L0 >= a.stop[b]);
-                if (!skip) {
-                    const int jj = L0 - a.T0;  // the new token's stream row: its page must exist (host invariant)
-                    const uint64_t pg = (jj >= 0 && (jj >> 5) < a.max_chunks) ? a.table[(int64_t)b * a.tstride + (jj >> 5)]
-                                                                               : 0;
-                    if (pg == 0 || (pg & 15u)) {
-                        st = 2;  // no page: poison the output (NaN logits the coder rejects), never write
-                    } else {
-                        st = 1;
-                        const int Lk = L0 + 1;
-                        s0 = a.window > 0 ? max(0, Lk - a.window) : 0;
-                        S = att_split(Lk - s0);
-                    }
+    // Every wave works out the workgroup's pairs itself (lane j < P: pair j's length, skip flags and new-token page;
+    // the same few loads in every wave hit the caches) -- no barrier before the streaming starts; the wave keeps
+    // them in its own LDS slots, not in registers.
+    int pr = -1, pL0 = 0, ps0 = 0, pS = 0, pst = 0;  // status 0 none / skipped, 1 run, 2 poison
+    if (lane < P) {
+        pr = att_pair<P>(blockIdx.x, lane, a.B, a.H);
+        if (pr >= 0) {
+            const int b = pr / a.H;
+            pL0 = a.lens[b];
+            const bool skip = (a.done && (a.done[(int64_t)b * a.done_stride] & 1u)) || (a.stop && pL0 >= a.stop[b]);
+            if (!skip) {
+                const int jj = pL0 - a.T0;  // the new token's stream row: its page must exist (host invariant)
+                const uint64_t pg =
+                    (jj >= 0 && (jj >> 5) < a.max_chunks) ? a.table[(int64_t)b * a.tstride + (jj >> 5)] : 0;
+                if (pg == 0 || (pg & 15u)) {
+                    pst = 2;  // no page: poison the output (NaN logits the coder rejects), never write
+                } else {
+                    pst = 1;
+                    const int Lk = pL0 + 1;
+                    ps0 = a.window > 0 ? max(0, Lk - a.window) : 0;
+                    pS = att_split(Lk - ps0);
                 }
             }
         }
-        int first = 0, total = 0;
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const int sk = __shfl(S, k);
-            first += k < lane ? sk : 0;
-            total += sk;
-        }
-        if (lane < P) {
-            s_info[lane][0] = pair;
-            s_info[lane][1] = L0;
-            s_info[lane][2] = s0;
-            s_info[lane][3] = S;
-            s_info[lane][4] = first;
-            s_info[lane][5] = st;
-        }
-        if (lane == 0) s_ntask = total;
     }
-    __syncthreads();
-    const int ntask = s_ntask;
+    int pfirst = 0, ntask = 0, multi = 0;  // task index of pair (lane)'s split 0; tasks; any pair split S > 1
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int sk = __shfl(pS, k);
+        pfirst += k < lane ? sk : 0;
+        ntask += sk;
+        multi |= sk > 1;
+    }
+    if (wave < P && __shfl(pst, wave) == 2) {  // poisoned pair: NaN rows
+        const int pair = __shfl(pr, wave);
+        a.out[(int64_t)(pair / a.H) * a.out_stride + (pair % a.H) * ATT_D + lane] = (_Float16)__builtin_nanf("");
+    }
+    if (lane < P) {
+        s_pi[wave][lane][0] = pr;
+        s_pi[wave][lane][1] = pL0;
+        s_pi[wave][lane][2] = ps0;
+        s_pi[wave][lane][3] = pfirst;
+    }
+    const int myS = wave < P ? __shfl(pS, wave) : 0;  // the merge phase's pair (wave) split
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS slots are written before they are read
+    __builtin_amdgcn_wave_barrier();
     const int g = lane / LPR;  // row within an RPI-row slab
     const int c = lane % LPR;  // DPL-dim slice
     const int C = a.H * ATT_D;
@@ -508,12 +519,13 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
         int j = 0;
 #pragma unroll
         for (int k = 1; k < P; ++k)
-            if (t >= s_info[k][4] && s_info[k][3] > 0) j = k;
-        const int pair = __builtin_amdgcn_readfirstlane(s_info[j][0]);
-        const int L0 = __builtin_amdgcn_readfirstlane(s_info[j][1]);
-        const int s0 = __builtin_amdgcn_readfirstlane(s_info[j][2]);
-        const int S = __builtin_amdgcn_readfirstlane(s_info[j][3]);
-        const int wv = t - __builtin_amdgcn_readfirstlane(s_info[j][4]);
+            if (t >= s_pi[wave][k][3]) j = k;  // the last pair whose first task is <= t (pairs without tasks share
+                                               // the next one's first task and are passed over)
+        const int pair = __builtin_amdgcn_readfirstlane(s_pi[wave][j][0]);
+        const int L0 = __builtin_amdgcn_readfirstlane(s_pi[wave][j][1]);
+        const int s0 = __builtin_amdgcn_readfirstlane(s_pi[wave][j][2]);
+        const int wv = t - __builtin_amdgcn_readfirstlane(s_pi[wave][j][3]);
+        const int S = att_split(L0 + 1 - s0);
         const int T0 = a.T0;
         const int Lk = L0 + 1;
         const int last_cached = L0 > 0 ? L0 - 1 : 0;
@@ -536,10 +548,26 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
         float acc[DPL];
 #pragma unroll
         for (int d = 0; d < DPL; ++d) acc[d] = 0.0f;
+        const int step = S * RPI * NI;
+        const int jbeg = s0 + wv * RPI * NI;
+        // page addresses of 64 iterations at a time, one per lane (lane i: iteration kbase + i; the first and the
+        // second page its 32 rows touch), read back with readlane: no dependent table load inside the stream
+        int kbase = -64;
+        uint64_t pgA = 0, pgB = 0;
+        auto pages_of = [&](int k, uint64_t& pa, uint64_t& pb) {
+            if (k - kbase >= 64) {
+                kbase = k;
+                const int jj = jbeg + (k + lane) * step - T0;
+                const bool in = jj >= 0 && jj + RPI * NI <= L0 - T0;  // an interior iteration: cached rows only
+                pgA = in ? trow[jj >> 5] : 0;
+                pgB = in && (jj & 31) ? trow[(jj >> 5) + 1] : pgA;
+            }
+            pa = readlane64(pgA, k - kbase);
+            pb = readlane64(pgB, k - kbase);
+        };
         // one iteration = RPI*NI = 32 consecutive rows from j0; GENERAL handles the prefix boundary, the clamp past
-        // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages, looked up
-        // once per iteration (wave-uniform)
-        auto load_chunk = [&](int j0, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
+        // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages
+        auto load_chunk = [&](int j0, int k, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
             constexpr bool GEN = decltype(general)::value;
             if constexpr (GEN) {
 #pragma unroll
@@ -555,10 +583,10 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
                     }
                 }
             } else {
+                uint64_t pa, pb;
+                pages_of(k, pa, pb);
                 const int jj0 = j0 - T0;
                 const int ca = jj0 >> 5;
-                const uint64_t pa = trow[ca];
-                const uint64_t pb = (jj0 & 31) ? trow[ca + 1] : pa;
 #pragma unroll
                 for (int u = 0; u < NI; ++u) {
                     const int jj = jj0 + RPI * u + g;
@@ -603,34 +631,34 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
             m = mx;
         };
         auto interior = [&](int j0) { return j0 >= T0 && j0 + RPI * NI <= L0; };
-        const int step = S * RPI * NI;
         Raw kr[NI], vr[NI];
-        int j0 = s0 + wv * RPI * NI;
         if constexpr (P > 1) {
-            for (; j0 < Lk; j0 += step) {
+            int k = 0;
+            for (int j0 = jbeg; j0 < Lk; j0 += step, ++k) {
                 if (interior(j0)) {
-                    load_chunk(j0, std::false_type{}, kr, vr);
+                    load_chunk(j0, k, std::false_type{}, kr, vr);
                     math_chunk(j0, std::false_type{}, kr, vr);
                 } else {
-                    load_chunk(j0, std::true_type{}, kr, vr);
+                    load_chunk(j0, k, std::true_type{}, kr, vr);
                     math_chunk(j0, std::true_type{}, kr, vr);
                 }
             }
         } else {  // one pair per workgroup (small batches): register double buffer, as the lockstep kernel
             Raw kn[NI], vn[NI];
+            int j0 = jbeg, k = 0;
             if (j0 < Lk) {
                 if (interior(j0))
-                    load_chunk(j0, std::false_type{}, kr, vr);
+                    load_chunk(j0, 0, std::false_type{}, kr, vr);
                 else
-                    load_chunk(j0, std::true_type{}, kr, vr);
+                    load_chunk(j0, 0, std::true_type{}, kr, vr);
             }
-            for (; j0 < Lk; j0 += step) {
+            for (; j0 < Lk; j0 += step, ++k) {
                 const int j1 = j0 + step;
                 if (j1 < Lk) {
                     if (interior(j1))
-                        load_chunk(j1, std::false_type{}, kn, vn);
+                        load_chunk(j1, k + 1, std::false_type{}, kn, vn);
                     else
-                        load_chunk(j1, std::true_type{}, kn, vn);
+                        load_chunk(j1, k + 1, std::true_type{}, kn, vn);
                 }
                 if (interior(j0))
                     math_chunk(j0, std::false_type{}, kr, vr);
@@ -657,7 +685,22 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
             }
             m = mn;
         }
-        if (g == 0) {
+        if (S == 1) {  // the whole pair in this wave: out = acc / l, as the lockstep kernel (a 1-way merge is exact)
+            if (g == 0) {
+                const float inv = 1.0f / l;
+#pragma unroll
+                for (int h8 = 0; h8 < DPL / 8; ++h8) {
+                    f16x8 o;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        float tv = acc[h8 * 8 + i] * inv;
+                        asm volatile("" : "+v"(tv));
+                        o[i] = (_Float16)tv;
+                    }
+                    *(f16x8*)(a.out + (int64_t)b * a.out_stride + h * ATT_D + c * DPL + h8 * 8) = o;
+                }
+            }
+        } else if (g == 0) {
 #pragma unroll
             for (int d = 0; d < DPL; ++d) s_acc[t][c * DPL + d] = acc[d];
             if (c == 0) {
@@ -666,19 +709,15 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
             }
         }
     }
+    if (!multi) return;  // uniform: no pair was split over waves
     __syncthreads();
-    if (wave >= P) return;
-    const int st = s_info[wave][5];
-    const int pair = s_info[wave][0];
-    if (st == 0) return;  // no pair, or skipped: the output row keeps its old (finite) values
+    // pair (wave) split over S > 1 waves: merge the S partials in split order, as the lockstep kernel does
+    if (wave >= P || lane >= LPR) return;
+    const int S = myS;
+    if (S <= 1) return;
+    const int w0 = s_pi[wave][wave][3];
+    const int pair = s_pi[wave][wave][0];
     const int b = pair / a.H, h = pair - b * a.H;
-    _Float16* orow = a.out + (int64_t)b * a.out_stride + h * ATT_D;
-    if (st == 2) {
-        orow[lane] = (_Float16)__builtin_nanf("");
-        return;
-    }
-    if (lane >= LPR) return;
-    const int S = s_info[wave][3], w0 = s_info[wave][4];
     float mt = s_m[w0];
     for (int w = 1; w < S; ++w) mt = fmaxf(mt, s_m[w0 + w]);
     float l = 0.0f;
@@ -701,7 +740,7 @@ __global__ __launch_bounds__(512) void paged_attn_kernel(const PagedArgs a) {
             asm volatile("" : "+v"(tv));
             o[i] = (_Float16)tv;
         }
-        *(f16x8*)(orow + lane * DPL + h8 * 8) = o;
+        *(f16x8*)(a.out + (int64_t)b * a.out_stride + h * ATT_D + lane * DPL + h8 * 8) = o;
     }
 }
 
@@ -968,12 +1007,13 @@ static int paged_attention(nsg::PagedArgs a, void* hip_stream) {
 }
 
 extern "C" int ns_decode_attention_paged(const void* d_qkv, int64_t qkv_stride, const uint64_t* d_page_table,
-                                         int64_t table_stride, int max_chunks, int layer, const void* d_k_prefix,
+                                         int64_t table_stride, int max_chunks, int64_t layer_offset,
+                                         const void* d_k_prefix,
                                          const void* d_v_prefix, int64_t prefix_h_stride, int T0, int B, int H, int D,
                                          const int32_t* d_lens, int window, int kv_format, const uint32_t* d_done,
                                          int64_t done_stride, const int32_t* d_stop, void* d_out, int64_t out_stride,
                                          float scale, void* hip_stream) {
-    if (!d_qkv || !d_page_table || !d_lens || !d_out || B <= 0 || H <= 0 || T0 < 0 || layer < 0 || window < 0)
+    if (!d_qkv || !d_page_table || !d_lens || !d_out || B <= 0 || H <= 0 || T0 < 0 || layer_offset < 0 || window < 0)
         return NS_ERR_CONFIG;
     if (D != nsg::ATT_D) return NS_ERR_UNSUPPORTED;
     if (kv_format != NS_KV_FP16 && kv_format != NS_KV_FP8) return NS_ERR_CONFIG;
@@ -993,7 +1033,8 @@ extern "C" int ns_decode_attention_paged(const void* d_qkv, int64_t qkv_stride, 
     a.tstride = table_stride;
     a.max_chunks = max_chunks;
     a.v_off = (int64_t)H * 32 * D;
-    a.layer_off = (int64_t)layer * 2 * a.v_off;
+    if (layer_offset % (16 / esz)) return NS_ERR_CONFIG;  // 16-byte rows
+    a.layer_off = layer_offset;
     a.kp = T0 > 0 ? d_k_prefix : d_qkv;
     a.vp = T0 > 0 ? d_v_prefix : d_qkv;
     a.ph = prefix_h_stride;

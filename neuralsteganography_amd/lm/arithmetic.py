@@ -456,7 +456,9 @@ class HipArithmeticLM:
             S = max(1, min(B, int(slots) if slots else self.max_batch))
             dec = SlotDecoder(self, self._coder(params, S), token_lists, context, slots=S, use_graph=bool(graphs),
                               compact=self.slot_compaction)
-            return dec.run()
+            out = dec.run()
+            self.last_decode_schedule = {"slots": S, "evictions": dec.evictions, "compactions": dec.compactions}
+            return out
         ctx = self._coder(params, B)
         sess = DecodeSession(ctx, token_lists)
         logits = self.lm.prefill(context, B, max(sess.T, 1) + 1)

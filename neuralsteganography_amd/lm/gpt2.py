@@ -122,6 +122,7 @@ class BatchedGPT2:
         # current call's page table + per-stream lengths
         self.pool = None
         self.kv = None
+        self.kv_segment_pages = None  # pages per pool segment (None: from the first call's batch)
         self.first_logits = None  # [1, ld] logits of the shared context (a refilled slot's first coder step)
         # optional per-stream done flags read by the decode attention (int32 tensor view [B], bit 0 = finished, e.g.
         # the coder state's flags word): finished streams skip their cache reads; their logits are never used again
@@ -487,13 +488,18 @@ class BatchedGPT2:
         free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         return int(free - 0.05 * total) - self.headroom_bytes(max(self.B, 1))
 
-    def page_pool(self):
+    def page_pool(self, B: int = 0):
+        """The page pool (created on first use; ``kv_segment_pages`` pages per segment, default from the first
+        call's batch: 2B rounded up to a power of two within [64, 1024])."""
         from .kvpages import KVPagePool
 
         if self.pool is None:
             s = self.shape
+            seg = self.kv_segment_pages
+            if seg is None:
+                seg = min(1024, max(64, 1 << max(0, 2 * int(B or self.B or 1) - 1).bit_length()))
             self.pool = KVPagePool(s.n_layer, s.n_head, s.n_embd // s.n_head, self.kv_torch_dtype, self.device,
-                                   budget_bytes=self._pool_budget)
+                                   budget_bytes=self._pool_budget, seg_pages=seg)
         return self.pool
 
     def begin_slots(self, B: int, T0: int, max_new: int = 32) -> None:
@@ -501,7 +507,7 @@ class BatchedGPT2:
         table (every page of the pool free again), no page assigned yet."""
         from .kvpages import PAGE_ROWS, PagedKV
 
-        pool = self.page_pool()
+        pool = self.page_pool(B)
         self.kv = None
         pool.reset()
         self.kv = PagedKV(pool, B, T0, (max(1, int(max_new)) + PAGE_ROWS - 1) // PAGE_ROWS + 1)
@@ -512,12 +518,13 @@ class BatchedGPT2:
         """Grow the page pool to ``pages`` pages (default: as many as the device budget allows at batch ``B``) and
         write every new page once, so a timed call finds its pages mapped and warm (a first pass over freshly
         allocated device memory measured up to 12 % slower per step).  Returns the pool's size in pages."""
-        pool = self.page_pool()
+        pool = self.page_pool(B)
         saveB, self.B = self.B, max(self.B, int(B))
         try:
             want = pool.total + pool.growable_pages() if pages is None else int(pages)
-            if want > pool.total:
-                pool.add_segment(min(want - pool.total, pool.growable_pages()))
+            while pool.total < want and pool.growable_pages() >= pool.seg_pages:  # a segment at a time, in budget
+                if not pool.add_segment(pool.seg_pages):
+                    break
             for seg in pool.segments:
                 seg.zero_()
         finally:
@@ -597,7 +604,7 @@ class BatchedGPT2:
             kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
             vp = self.vp[i, 0] if T0 else None
             rc = L.ns_decode_attention_paged(qkv.data_ptr(), qkv.stride(0), kv.table.data_ptr(), kv.table.stride(0),
-                                             kv.width, i, kp.data_ptr() if T0 else None,
+                                             kv.width, kv.pool.layer_offset(i), kp.data_ptr() if T0 else None,
                                              vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D,
                                              lens, self.window, self._kv_format, done_ptr, done_stride, stop_ptr,
                                              o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)

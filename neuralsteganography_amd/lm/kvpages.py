@@ -5,8 +5,13 @@ The reference keeps one unbounded KV cache per message and runs every message in
 caches of different, unknown lengths.  A dense ``[B, longest]`` allocation wastes the memory of every short
 stream and must be copied to grow; here a stream's rows live in pages it owns:
 
-* a PAGE holds 32 positions of one stream for every layer, ``[layer][K|V][H][32][D]`` in the cache's element type
-  (1.18 MB for GPT-2-small fp16), so the attention of one (stream, head) reads 4 KiB contiguous per page and layer;
+* a PAGE holds 32 positions of one stream for every layer, ``[K|V][H][32][D]`` per layer in the cache's element
+  type (1.18 MB for GPT-2-small fp16 over its 12 layers), so the attention of one (stream, head) reads 4 KiB
+  contiguous per page and layer; pages live in SEGMENTS of ``seg_pages`` pages stored layer-major,
+  ``[layer][page][K|V][H][32][D]``, so one layer's pages are contiguous (a decode step's attention walks one layer
+  at a time: as few address-translation regions per launch as the dense cache had -- pages that interleave the
+  layers measured 3-22 % slower, ``tools/paged_attn_probe.py``); a page's table entry is its layer-0 block's
+  address and layer ``i`` is ``i * seg_pages * block`` elements further;
 * the page TABLE ``[B, width]`` (uint64 device addresses, 0 = none) maps a stream's row ``r`` (position ``T0 + r``)
   to page ``table[b, r // 32]`` -- ``ns_decode_attention_paged`` reads it; per-stream cache lengths ``lens[B]``
   (int32, device) feed the position embedding and the attention and are advanced by the step's final layer norm;
@@ -30,25 +35,32 @@ PAGE_ROWS = 32
 
 
 class KVPagePool:
-    """Pages of ``page_elems`` elements in segments of device memory; a free list of page addresses.
+    """Pages in layer-major segments of ``seg_pages`` pages each; a free list of page (layer-0 block) addresses.
 
     ``budget_bytes()`` says how much more device memory the pool may take (free memory minus what the caller must
-    keep free); growth asks for ``max(needed, total / 4, min_segment)`` pages within that budget."""
+    keep free); growth asks for ``max(needed, total / 4)`` pages, in whole segments, within that budget."""
 
     def __init__(self, n_layer: int, n_head: int, head_dim: int, dtype: torch.dtype, device,
-                 budget_bytes: Optional[Callable[[], int]] = None, min_segment: int = 256):
-        self.page_elems = n_layer * 2 * n_head * PAGE_ROWS * head_dim
+                 budget_bytes: Optional[Callable[[], int]] = None, seg_pages: int = 1024):
+        self.n_layer = int(n_layer)
+        self.block_elems = 2 * n_head * PAGE_ROWS * head_dim  # one layer's [K|V][H][32][D]
+        self.page_elems = self.n_layer * self.block_elems
         self.esize = torch.tensor([], dtype=dtype).element_size()
+        self.block_bytes = self.block_elems * self.esize
         self.page_bytes = self.page_elems * self.esize
         self.dtype, self.device = dtype, torch.device(device)
         self.budget_bytes = budget_bytes
-        self.min_segment = int(min_segment)
+        self.seg_pages = max(1, int(seg_pages))
         self.segments: List[torch.Tensor] = []
         self._free = np.empty(0, dtype=np.int64)
         self._nfree = 0
         self.total = 0
 
     # ------------------------------------------------------------------
+    def layer_offset(self, layer: int) -> int:
+        """Elements from a page's address to its block of ``layer`` (``ns_decode_attention_paged``)."""
+        return int(layer) * self.seg_pages * self.block_elems
+
     @property
     def free_pages(self) -> int:
         return self._nfree
@@ -58,20 +70,26 @@ class KVPagePool:
             return 1 << 40
         return max(0, int(self.budget_bytes()) // self.page_bytes)
 
+    def _addresses(self, seg: torch.Tensor) -> np.ndarray:
+        return seg.data_ptr() + self.block_bytes * np.arange(self.seg_pages, dtype=np.int64)
+
     def add_segment(self, npages: int) -> bool:
-        """Map ``npages`` more pages (one allocation); False if the device cannot hold them."""
-        npages = int(npages)
-        if npages <= 0:
+        """Map at least ``npages`` more pages (whole segments, one allocation each); False (nothing mapped) if the
+        device cannot hold them."""
+        nseg = -(-int(npages) // self.seg_pages)
+        if nseg <= 0:
             return False
-        try:
-            seg = torch.empty((npages, self.page_elems), dtype=self.dtype, device=self.device)
-        except torch.OutOfMemoryError:
-            return False
-        base = seg.data_ptr()
-        addrs = base + self.page_bytes * np.arange(npages, dtype=np.int64)
-        self.segments.append(seg)
-        self._push(addrs[::-1])  # pages are taken from the top: lowest addresses first
-        self.total += npages
+        new = []
+        for _ in range(nseg):
+            try:
+                new.append(torch.empty((self.n_layer, self.seg_pages, self.block_elems), dtype=self.dtype,
+                                       device=self.device))
+            except torch.OutOfMemoryError:
+                return False
+        for seg in new:
+            self.segments.append(seg)
+            self._push(self._addresses(seg)[::-1])  # pages are taken from the top: lowest addresses first
+            self.total += self.seg_pages
         return True
 
     def _push(self, addrs: np.ndarray) -> None:
@@ -90,10 +108,10 @@ class KVPagePool:
             return np.empty(0, dtype=np.int64)
         if self._nfree < n:
             short = n - self._nfree
-            room = self.growable_pages()
+            room = self.growable_pages() // self.seg_pages * self.seg_pages
             if room < short:
                 return None
-            want = min(room, max(short, self.total // 4, self.min_segment))
+            want = min(room, max(short, self.total // 4))
             if not self.add_segment(want) and not (want > short and self.add_segment(short)):
                 return None
         out = self._free[self._nfree - n: self._nfree][::-1].copy()
@@ -110,8 +128,7 @@ class KVPagePool:
         self._free = np.empty(0, dtype=np.int64)
         self._nfree = 0
         for seg in self.segments:
-            base = seg.data_ptr()
-            self._push((base + self.page_bytes * np.arange(seg.shape[0], dtype=np.int64))[::-1])
+            self._push(self._addresses(seg)[::-1])
 
     def release_memory(self) -> None:
         self.segments = []

@@ -273,8 +273,8 @@ class SlotEncoder:
 
 
 class SlotDecoder:
-    """Decode ``token_lists`` through ``slots`` slots: every message's tokens are known, so admission maps all of a
-    message's pages up front (no eviction) and a slot's end is known on the host (no state read to find it)."""
+    """Decode ``token_lists`` through ``slots`` slots, longest first: pages are mapped as the streams grow (as the
+    encoder maps them, with the same eviction), and a slot's end is known on the host from its token count."""
 
     def __init__(self, provider, ctx, token_lists: Sequence[Sequence[int]], context: Sequence[int], *, slots: int,
                  use_graph: bool, check_every: int = 16, compact: bool = True):
@@ -285,6 +285,7 @@ class SlotDecoder:
         self.context = context
         self.use_graph, self.check_every, self.allow_compact = use_graph, int(check_every), compact
         self.compactions = 0
+        self.evictions = 0
 
     def run(self) -> List[List[int]]:
         import torch
@@ -318,6 +319,7 @@ class SlotDecoder:
         p = self.ctx.params
         graph, gkey = None, None
         bufs = {}
+        admit_blocked = False
 
         def body():
             tix = lm.kv.lens - T0
@@ -353,29 +355,41 @@ class SlotDecoder:
                         lm.kv.release(fin)
                         slot_msg[fin] = -1
                         nlen_host[fin] = 0
+                        admit_blocked = False
                         fi = torch.as_tensor(fin, device=dev)
                         st["nlen"][fi] = 0
                         st["stop"][fi] = 0
                         live = slot_msg >= 0
                     empty = np.nonzero(~live)[0]
-                    adm_s, adm_m = [], []
-                    for s in empty.tolist():
-                        if not queue:
+                    if queue and empty.size and not admit_blocked:
+                        room = lm.pool.free_pages + lm.pool.growable_pages() - int(live.sum()) - 1
+                        n_adm = int(min(empty.size, len(queue), max(0, room)))
+                        if n_adm:
+                            adm_s = empty[:n_adm]
+                            adm_m = [queue.popleft() for _ in range(n_adm)]
+                            lm.kv.reset(adm_s)
+                            self._admit(st, logits, first, init_row, adm_s, adm_m, slot_msg, nlen_host, T0, Tcap)
+                            live = slot_msg >= 0
+                    # pages for the next check_every + 1 positions (never past a message's last fed token); on a full
+                    # device the youngest messages go back to the queue's front (re-decoded later: the same bits)
+                    while live.any():
+                        sl = np.nonzero(live)[0]
+                        upto = np.minimum(lm.kv.lens_host[sl] + self.check_every + 1, T0 + nlen_host[sl])
+                        if lm.kv.ensure(sl, upto).size == 0:
                             break
-                        m = queue[0]
-                        n = int(lens_all[m])
-                        lm.kv.reset([s])
-                        if lm.kv.ensure([s], T0 + n).size:
-                            if not live.any() and not adm_s:
-                                raise KVCapacityError(f"message {m} ({n} tokens) needs more KV pages than the "
-                                                      "device holds")
-                            break
-                        queue.popleft()
-                        adm_s.append(s)
-                        adm_m.append(m)
-                    if adm_s:
-                        self._admit(st, logits, first, init_row, adm_s, adm_m, slot_msg, nlen_host, T0, Tcap)
+                        if sl.size == 1:
+                            raise KVCapacityError(f"message {int(slot_msg[sl[0]])} ({int(nlen_host[sl[0]])} tokens) "
+                                                  "needs more KV pages than the device holds")
+                        v = sl[np.argmin(lm.kv.lens_host[sl])]
+                        queue.appendleft(int(slot_msg[v]))
+                        lm.kv.release([v])
+                        vi = torch.as_tensor([int(v)], device=dev)
+                        st["nlen"][vi] = 0
+                        st["stop"][vi] = 0
+                        slot_msg[v], nlen_host[v] = -1, 0
                         live = slot_msg >= 0
+                        admit_blocked = True
+                        self.evictions += 1
                     if not live.any():
                         break
                     if self.allow_compact and not queue and int(live.sum()) <= st["state"].shape[0] // 2 and \

@@ -238,6 +238,28 @@ def test_fraction_table_growth_in_a_mixed_batch(F):
         assert d == payloads[b], b
 
 
+def test_fraction_scratch_budget_splits_a_group_instead_of_failing_it(F, monkeypatch):
+    """streams whose grown tables do not fit the scratch budget TOGETHER are launched in chunks
+    that do (each fits alone), so every message still gets the restatement's tokens -- a message never fails because
+    of what else is in its batch."""
+    rng = np.random.default_rng(12)
+    streams = [[(lambda p: p / p.sum())(rng.random(300)) for _ in range(30)] for _ in range(6)]
+    payloads = [bytes([b, 7]) for b in range(6)]
+    dv = F._Device(1, F.DEFAULT_CAP_LIMBS)
+    one = int(dv.L.ns_frac_scratch_bytes(dv.ctx, 1, 300, 16, 8 * F.DEFAULT_TABLE_LIMBS))
+    dv.close()
+    assert one > 0
+    monkeypatch.setattr(F, "SCRATCH_BUDGET_BYTES", one * 3 // 2)  # grown tables: one stream per launch
+    got = F.encode_bits_batch(payloads, [iter(s) for s in streams], [{} for _ in payloads], return_exceptions=True)
+    for b, (payload, ds, g) in enumerate(zip(payloads, streams, got)):
+        want = _oracle_encode(payload, ds)
+        if isinstance(want, tuple) and isinstance(want[0], str):
+            assert isinstance(g, Exception) and _kind(g) == want, (b, g, want)
+        else:
+            assert g == want[0], b
+    assert sum(not isinstance(g, Exception) for g in got) >= 3
+
+
 def test_fraction_capacity_is_per_message(F):
     """an interval arena too small for one message's lcm (NS_FRAC_ERR_CAPACITY, which no table
     can cure) fails that message only, with FractionCapacityError, without growing any table."""

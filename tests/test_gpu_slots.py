@@ -74,7 +74,8 @@ def _run_paged(c, B, window=0, done=None, stop=None, table=None):
     tab = c["table"] if table is None else table
     T0 = c["T0"]
     rc = _lib.lib().ns_decode_attention_paged(
-        c["qkv"].data_ptr(), c["qkv"].stride(0), tab.data_ptr(), tab.stride(0), tab.shape[1], c["layer"],
+        c["qkv"].data_ptr(), c["qkv"].stride(0), tab.data_ptr(), tab.stride(0), tab.shape[1],
+        c["layer"] * 2 * H * 32 * D,
         c["kp"].data_ptr() if T0 else None, c["vp"].data_ptr() if T0 else None, c["kp"].stride(0) if T0 else 0, T0, B,
         H, D, c["lens"].data_ptr(), window, c["fmt"], done.data_ptr() if done is not None else None,
         done.stride(0) if done is not None else 0, stop.data_ptr() if stop is not None else None, out.data_ptr(),
@@ -215,6 +216,7 @@ def test_eviction_when_the_pool_is_small_gives_the_same_tokens():
     ref = ref_lm.encode_batch(bits, ctx, quality=Q)
     del ref_lm
     lm = _provider(seed=43)
+    lm.lm.kv_segment_pages = 1  # a page-exact budget
     pool = lm.lm.page_pool()
     cap_pages = 14  # far fewer than 8 live covers of ~80-150 tokens need at their peak
     pool.budget_bytes = lambda: (cap_pages - pool.total) * pool.page_bytes
@@ -230,6 +232,7 @@ def test_kv_capacity_error_not_torch_oom():
     from neuralsteganography_amd.exceptions import KVCapacityError
 
     lm = _provider(seed=44)
+    lm.lm.kv_segment_pages = 1  # a page-exact budget
     pool = lm.lm.page_pool()
     pool.budget_bytes = lambda: (2 - pool.total) * pool.page_bytes  # 2 pages: 64 positions per message at most
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(5, 200))]

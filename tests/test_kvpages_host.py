@@ -8,36 +8,44 @@ import torch
 from neuralsteganography_amd.lm.kvpages import PAGE_ROWS, KVPagePool, PagedKV
 
 
-def _pool(budget_pages=None, min_segment=4):
+def _pool(budget_pages=None, seg_pages=4):
     holder = {}
     budget = None
     if budget_pages is not None:
         def budget():
             return (budget_pages - holder["pool"].total) * holder["pool"].page_bytes
     pool = KVPagePool(n_layer=2, n_head=2, head_dim=64, dtype=torch.float16, device="cpu", budget_bytes=budget,
-                      min_segment=min_segment)
+                      seg_pages=seg_pages)
     holder["pool"] = pool
     return pool
 
 
 def test_page_geometry_and_addresses():
-    pool = _pool()
-    assert pool.page_elems == 2 * 2 * 2 * PAGE_ROWS * 64 and pool.page_bytes == 2 * pool.page_elems
+    pool = _pool(seg_pages=8)
+    assert pool.block_elems == 2 * 2 * PAGE_ROWS * 64 and pool.page_elems == 2 * pool.block_elems
+    assert pool.page_bytes == 2 * pool.page_elems
     pages = pool.take(5)
     assert pages.size == 5 and len(set(pages.tolist())) == 5
     seg = pool.segments[0]
+    assert tuple(seg.shape) == (2, 8, pool.block_elems)  # layer-major: [layer][page][block]
     base = seg.data_ptr()
-    for a in pages.tolist():  # every address is a page boundary inside a segment
-        assert (a - base) % pool.page_bytes == 0 and 0 <= (a - base) // pool.page_bytes < seg.shape[0]
-    assert all(a % 16 == 0 for a in pages.tolist())
+    for a in pages.tolist():  # every address is a layer-0 block inside the segment
+        assert (a - base) % pool.block_bytes == 0 and 0 <= (a - base) // pool.block_bytes < 8
+        assert a % 16 == 0
+    # layer 1 of a page is layer_offset(1) elements after its address: the same page index in the second layer plane
+    i = (int(pages[2]) - base) // pool.block_bytes
+    flat = seg.view(-1)
+    off = (int(pages[2]) - base) // pool.esize + pool.layer_offset(1)
+    flat[off] = 7.0
+    assert seg[1, i, 0].item() == 7.0
 
 
 def test_take_give_reuses_pages_and_grows_by_segments():
-    pool = _pool(min_segment=4)
+    pool = _pool(seg_pages=4)
     a = pool.take(3)
     assert pool.total == 4 and pool.free_pages == 1
-    b = pool.take(6)  # grows: max(short, total/4, min_segment)
-    assert pool.total >= 9 and len(pool.segments) == 2
+    b = pool.take(6)  # grows by whole segments: max(short, total/4) pages, rounded up
+    assert pool.total >= 9 and pool.total % 4 == 0 and len(pool.segments) >= 2
     pool.give(a)
     c = pool.take(3)
     assert set(c.tolist()) == set(a.tolist())  # freed pages come back first
@@ -45,13 +53,15 @@ def test_take_give_reuses_pages_and_grows_by_segments():
 
 
 def test_budget_limits_growth_and_failure_takes_nothing():
-    pool = _pool(budget_pages=10, min_segment=4)
+    pool = _pool(budget_pages=10, seg_pages=1)
     assert pool.take(8) is not None
     free_before = pool.free_pages
     assert pool.take(5) is None  # 8 used + 5 > 10
     assert pool.free_pages == free_before
     assert pool.take(2) is not None
     assert pool.total <= 10
+    seg4 = _pool(budget_pages=10, seg_pages=4)
+    assert seg4.take(8) is not None and seg4.take(1) is None  # a third segment of 4 would pass the budget
 
 
 def test_ensure_maps_pages_in_order_and_mirrors_the_device_table():
@@ -82,7 +92,7 @@ def test_release_reset_and_steps_reserved():
 
 
 def test_ensure_reports_slots_the_pool_cannot_serve():
-    pool = _pool(budget_pages=5, min_segment=1)
+    pool = _pool(budget_pages=5, seg_pages=1)
     kv = PagedKV(pool, B=3, T0=0, width=8)
     failed = kv.ensure([0, 1, 2], [64, 64, 64])  # 2 pages each, 5 available: slot 2 fails, nothing half-mapped
     assert failed.tolist() == [2]
