@@ -274,7 +274,7 @@ def test_graph_captured_encode_matches_eager(cap_pages, topk, n):
         lm = HipArithmeticLM(m, None, logits_dtype="f16")
         if cap_pages is not None:
             lm.lm.kv_segment_pages = 1  # a page-exact budget
-    pool = lm.lm.page_pool()
+            pool = lm.lm.page_pool()
             pool.budget_bytes = lambda: (cap_pages - pool.total) * pool.page_bytes
         out[graphs] = lm.encode_batch(bits, ctx, quality=q, graphs=graphs)
         dec = lm.decode_batch(out[graphs], ctx, quality=q, graphs=graphs)
