@@ -242,14 +242,14 @@ def _wide_traffic(B):
     from neuralsteganography_amd import _lib
 
     ver = _lib.version()
-    for path in sorted(glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_wide_onepass_*.json"))):
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "r0[56]" / "pmc_traffic_wide_onepass_*.json"))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
         if rec.get("library_version") == ver:
-            return rec["traffic_bytes_per_launch"] * B / rec["batch"]
-    return None
+            return rec["traffic_bytes_per_launch"] * B / rec["batch"], "from " + str(Path(path).relative_to(ROOT))
+    return None, None
 
 
 def wide_path(args, rank, world, dev, steps=10, warmup=3):
@@ -297,6 +297,7 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
     ntok = int(f["ntokens"].astype("int64").sum() - nt0)
     bits_all, tok_all, el_max, _ = reduce_job(nbits, ntok, elapsed, 0.0, device=dev)
     alg = B * (V * 4 + 76)  # the row read once + state/token/payload window, per step
+    wtr = _wide_traffic(B)
     del pool, sess, ctx
     torch.cuda.empty_cache()
     return {"value": bits_all / el_max, "unit": "payload bits/s", "cover_tokens_per_s": tok_all / el_max,
@@ -304,20 +305,22 @@ def wide_path(args, rank, world, dev, steps=10, warmup=3):
             "achieved_gbs": alg / (el_max / steps) / 1e9, "peak_gbs": HBM_PEAK_GBS,
             "frac": alg / (el_max / steps) / 1e9 / HBM_PEAK_GBS,
             "listed_stream_step_fraction": (c1[0] - c0[0]) / max(ntok, 1),
-            "traffic": _wide_traffic(B),
+            "traffic": wtr[0], "traffic_source": wtr[1],
             "workload": f"api default quality: {B} streams/GPU x ns_encode_step, precision 16, topk 50000, temp 1.0, "
                         f"resident [{B},{ld}] f32 3N(0,1) logits, {args.payload_bytes}-byte payloads"}
 
 
 def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3, T0=32):
-    """The decode attention of the headline's step alone (``ns_decode_attention_prefix``, ``decode_attn_kernel``:
+    """The decode attention of the headline's step alone (``ns_decode_attention_paged``, ``paged_attn_kernel``:
     ~80 % of the C3 step): one GPT-2-small layer at the e2e batch, the shared 32-position context stored once and
-    each stream's own rows in chunk planes, cache length ``L`` (default: the C3 job's mean attended length), random
-    fp16 K/V/q.  K launches timed with HIP events on the launch stream.  Algorithmic bytes per launch (DESIGN
-    §4b): B·H·(L+1−T0)·2·D·2 (each stream's K and V rows, the new one included) + H·T0·2·D·2 (the shared prefix)
-    + B·3C·2 (qkv) + B·C·2 (out).  Returns the ``roofline_attention`` object."""
+    each stream's own rows in 32-position pages of a layer-major pool segment, mapped chunk by chunk over the streams
+    as the slot scheduler maps them, every stream at cache length ``L`` (default: the C3 job's mean attended
+    length), random fp16 K/V/q.  K launches timed with HIP events on the launch stream.  Algorithmic bytes per launch
+    (DESIGN §4b): B·H·(L+1−T0)·2·D·2 (each stream's K and V rows, the new one included) + H·T0·2·D·2 (the shared
+    prefix) + B·3C·2 (qkv) + B·C·2 (out).  Returns the ``roofline_attention`` object."""
     import math
 
+    import numpy as np
     import torch
 
     from neuralsteganography_amd import _lib
@@ -328,26 +331,29 @@ def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3, T0=32):
     L = int(L or 544)
     rows = L + 1 - T0
     nch = (rows + 31) // 32
+    blk = 2 * H * 32 * D  # one layer's [K|V][H][32][D] block of a page
+    npages = B * nch
     g = torch.Generator(device=dev)
     g.manual_seed(77 + rank)
-    kc = torch.randn((nch, B, H, 32, D), generator=g, device=dev, dtype=torch.float16)
-    vc = torch.randn((nch, B, H, 32, D), generator=g, device=dev, dtype=torch.float16)
+    pool = torch.randn((npages, blk), generator=g, device=dev, dtype=torch.float16)  # one layer plane of a segment
     kp = torch.randn((H, T0, D), generator=g, device=dev, dtype=torch.float16)
     vp = torch.randn((H, T0, D), generator=g, device=dev, dtype=torch.float16)
     qkv = torch.randn((B, 3 * C), generator=g, device=dev, dtype=torch.float16)
     out = torch.empty((B, C), device=dev, dtype=torch.float16)
+    order = np.arange(npages, dtype=np.int64).reshape(nch, B).T  # page of (stream b, chunk c) = c * B + b
+    table = torch.from_numpy(np.ascontiguousarray(pool.data_ptr() + 2 * blk * order)).to(dev)
+    lens = torch.full((B,), L, dtype=torch.int32, device=dev)
     lib = _lib.lib()
     st = _stream_handle()
     stream = torch.cuda.current_stream()
 
     def launch():
-        rc = lib.ns_decode_attention_prefix(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), kc.stride(1),
-                                            kc.stride(2), kc.stride(0), kp.data_ptr() if T0 else None,
-                                            vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0,
-                                            B, H, D, L, None, T0 + nch * 32, 0, out.data_ptr(), out.stride(0),
-                                            1.0 / math.sqrt(D), st)
+        rc = lib.ns_decode_attention_paged(qkv.data_ptr(), qkv.stride(0), table.data_ptr(), table.stride(0), nch, 0,
+                                           kp.data_ptr(), vp.data_ptr(), kp.stride(0), T0, B, H, D, lens.data_ptr(), 0,
+                                           _lib.NS_KV_FP16, None, 0, None, out.data_ptr(), out.stride(0),
+                                           1.0 / math.sqrt(D), st)
         if rc != 0:
-            raise RuntimeError(f"ns_decode_attention_prefix failed ({rc})")
+            raise RuntimeError(f"ns_decode_attention_paged failed ({rc})")
 
     for _ in range(warmup):
         launch()
@@ -363,13 +369,14 @@ def attention_bench(args, rank, world, dev, L=None, steps=20, warmup=3, T0=32):
         raise RuntimeError("attention bench: non-finite output")
     alg = B * H * rows * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * C * 2 + B * C * 2
     achieved = alg / (kern_ms / 1e3) / 1e9
-    del kc, vc, kp, vp, qkv, out
+    del pool, kp, vp, qkv, out, table
     torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None, "kernel": "decode_attn_kernel<FmtF16,8> (ns_decode_attention_prefix)",
+            "traffic": None, "kernel": "paged_attn_kernel<FmtF16,8> (ns_decode_attention_paged)",
             "kernel_ms_avg": kern_ms, "launches": steps, "alg_bytes_per_launch": alg,
             "workload": f"one GPT-2-small layer, {B} streams x {H} heads, cache length L = {L} (T0 = {T0} shared "
-                        f"context positions + {rows} own rows incl. the new one, chunk planes), fp16",
+                        f"context positions + {rows} own rows incl. the new one, 32-position pages of a layer-major "
+                        "segment), fp16",
             "alg_bytes_formula": "B*H*(L+1-T0)*2*D*2 + H*T0*2*D*2 + B*3C*2 + B*C*2",
             "timing": "K eager launches between two HIP events on the launch stream"}
 
@@ -579,14 +586,16 @@ def measured_traffic(args, version):
     import glob
 
     best = None
-    for path in sorted(glob.glob(str(ROOT / "profiles" / "pmc_traffic_*.json")) + glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_*.json"))):
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "pmc_traffic_*.json")) +
+                       glob.glob(str(ROOT / "profiles" / "r0[56]" / "pmc_traffic_*.json"))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
         if (rec.get("library_version") == version and rec.get("batch") == args.batch and rec.get("vocab") == args.vocab
                 and rec.get("dtype") == args.dtype and rec.get("topk") == args.topk):
-            best = (rec["traffic_bytes_per_launch"], Path(path).name)
+            best = (rec["traffic_bytes_per_launch"], "from " + str(Path(path).relative_to(ROOT)) +
+                    " (committed rocprofv3 PMC record of this library build; not measured in this run)")
     return best
 
 
@@ -598,7 +607,7 @@ def _attn_traffic(args, L):
     from neuralsteganography_amd import _lib
 
     ver = _lib.version()
-    for path in sorted(glob.glob(str(ROOT / "profiles" / "r05" / "pmc_traffic_attn*.json"))):
+    for path in sorted(glob.glob(str(ROOT / "profiles" / "r0[56]" / "pmc_traffic_attn*.json"))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
@@ -607,7 +616,9 @@ def _attn_traffic(args, L):
             per_row = rec["traffic_bytes_per_launch"] / rec["alg_bytes_per_launch"]
             B, H, D, T0 = args.e2e_batch, 12, 64, 32
             alg = B * H * (L + 1 - T0) * 2 * D * 2 + H * T0 * 2 * D * 2 + B * 3 * H * D * 2 + B * H * D * 2
-            return per_row * alg, f"{Path(path).name} (traffic/alg ratio {per_row:.3f} at L = {rec['L']})"
+            return per_row * alg, (f"from {Path(path).relative_to(ROOT)} (committed rocprofv3 PMC record of this "
+                                   f"library build, traffic/alg ratio {per_row:.3f} at L = {rec['L']}; not measured in "
+                                   "this run)")
     return None, None
 
 

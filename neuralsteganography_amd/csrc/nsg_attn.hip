@@ -551,16 +551,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         const int step = S * RPI * NI;
         const int jbeg = s0 + wv * RPI * NI;
         // page addresses of 64 iterations at a time, one per lane (lane i: iteration kbase + i; the first and the
-        // second page its 32 rows touch), read back with readlane: no dependent table load inside the stream
+        // last page of the stream rows it reads -- rows past the cache are clamped to the last cached one), read
+        // back with readlane: no dependent table load inside the stream
+        const int hi_row = last_cached - T0;  // the last stream row an iteration reads (< 0: prefix rows only)
         int kbase = -64;
         uint64_t pgA = 0, pgB = 0;
         auto pages_of = [&](int k, uint64_t& pa, uint64_t& pb) {
             if (k - kbase >= 64) {
                 kbase = k;
                 const int jj = jbeg + (k + lane) * step - T0;
-                const bool in = jj >= 0 && jj + RPI * NI <= L0 - T0;  // an interior iteration: cached rows only
-                pgA = in ? trow[jj >> 5] : 0;
-                pgB = in && (jj & 31) ? trow[(jj >> 5) + 1] : pgA;
+                // rows read: [jj, jj + 31] clamped to the last cached row (as load_chunk clamps them); stream rows
+                // only (< 0: the shared prefix); beyond the job's iterations the lane loads nothing
+                const int lo = max(min(jj, hi_row), 0), hi = min(jj + RPI * NI - 1, hi_row);
+                const bool any = hi >= 0 && jj <= L0 - T0;
+                pgA = any ? trow[lo >> 5] : 0;
+                pgB = any && (hi >> 5) != (lo >> 5) ? trow[hi >> 5] : pgA;
             }
             pa = readlane64(pgA, k - kbase);
             pb = readlane64(pgB, k - kbase);
@@ -569,7 +574,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages
         auto load_chunk = [&](int j0, int k, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
             constexpr bool GEN = decltype(general)::value;
+            uint64_t pa, pb;
+            pages_of(k, pa, pb);
             if constexpr (GEN) {
+                const int ca = max(min(j0 - T0, hi_row), 0) >> 5;  // the chunk of the first stream row read (pa)
 #pragma unroll
                 for (int u = 0; u < NI; ++u) {
                     const int row = min(j0 + RPI * u + g, last_cached);
@@ -577,14 +585,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
                         kr[u] = att_load((const Raw*)(kpb + (int64_t)row * ATT_D));
                         vr[u] = att_load((const Raw*)(vpb + (int64_t)row * ATT_D));
                     } else {
-                        const E* ka = kaddr(trow[(row - T0) >> 5], row - T0);
+                        const int jj = row - T0;
+                        const E* ka = kaddr((jj >> 5) == ca ? pa : pb, jj);
                         kr[u] = att_load((const Raw*)ka);
                         vr[u] = att_load((const Raw*)(ka + a.v_off));
                     }
                 }
             } else {
-                uint64_t pa, pb;
-                pages_of(k, pa, pb);
                 const int jj0 = j0 - T0;
                 const int ca = jj0 >> 5;
 #pragma unroll
