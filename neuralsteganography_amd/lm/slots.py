@@ -59,6 +59,43 @@ def _layout_key(*tensors) -> tuple:
     return tuple(t.data_ptr() if t is not None else 0 for t in tensors)
 
 
+class _Pinned:
+    """Double-buffered pinned host copies of a device tensor, taken asynchronously on the current stream with an
+    event (the check pipeline of the slot loops: a check reads the PREVIOUS check's copy, whose event the GPU has
+    passed, while the steps enqueued since keep it busy)."""
+
+    def __init__(self):
+        self.bufs = [None, None]
+        self.k = 0
+
+    def take(self, dev_tensor):
+        import torch
+
+        b = self.bufs[self.k]
+        if b is None or b.shape != dev_tensor.shape or b.dtype != dev_tensor.dtype:
+            b = self.bufs[self.k] = torch.empty(dev_tensor.shape, dtype=dev_tensor.dtype, pin_memory=True)
+        b.copy_(dev_tensor, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.k ^= 1
+        return b, ev
+
+
+def _rows_after(event, side, tensor, rows, ncols=None):
+    """``tensor[rows, :ncols]`` on the host, gathered on the ``side`` stream once ``event`` has passed (rows that no
+    later step writes: finished streams), without waiting for the steps enqueued on the main stream since."""
+    import torch
+
+    with torch.cuda.stream(side):
+        side.wait_event(event)
+        idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=tensor.device)
+        out = tensor.index_select(0, idx)
+        if ncols is not None:
+            out = out[:, :ncols]
+        host = out.cpu()
+    return host
+
+
 class SlotEncoder:
     """Encode ``bit_lists`` through ``slots`` slots of ``provider.lm`` (a native :class:`BatchedGPT2`)."""
 
@@ -115,6 +152,13 @@ class SlotEncoder:
         def done_view():
             return sess.state.view(torch.int32)[:, 7] if skip else None
 
+        # check pipeline (graph replays, no per-step stop test): a check processes the coder states copied at the
+        # PREVIOUS check while the steps enqueued since run -- the GPU never waits for the host; a finished slot is
+        # seen one period later (it idles through it, skipping its attention) and its tokens are gathered on a side
+        # stream.  Eager or stop-text loops read the states synchronously.
+        pipelined = self.use_graph and stop is None
+        pin, pending = _Pinned(), None
+        side = torch.cuda.Stream() if pipelined else None
         lm.begin_static(logits)
         lm.done_flags = done_view()
         try:
@@ -122,9 +166,15 @@ class SlotEncoder:
                 if stop is not None and t > 0:
                     stop.check()
                 if t % self.check_every == 0:
-                    f = sess.fields()
+                    if pipelined:
+                        f, ev = (None, None) if pending is None else (pending[0], pending[1])
+                        if ev is not None:
+                            ev.synchronize()
+                            f = _state_fields(f)
+                    else:
+                        f, ev = sess.fields(), None
                     live = slot_msg >= 0
-                    flags = f["flags"]
+                    flags = f["flags"] if f is not None else np.zeros(sess.B, dtype=np.uint32)
                     # ---- harvest finished slots
                     fin = np.nonzero(live & ((flags & _lib.NS_ST_DONE) != 0))[0]
                     if fin.size:
@@ -135,10 +185,14 @@ class SlotEncoder:
                         nt = f["ntokens"][fin]
                         if int(nt.max(initial=0)) > sess.hist.shape[1]:
                             raise RuntimeError("token history overflow")
-                        rows = sess.hist[torch.as_tensor(fin, device=sess.hist.device), : max(1, int(nt.max()))]
-                        host = rows.cpu().numpy()
-                        acc = sess.stats_acc[torch.as_tensor(fin, device=sess.hist.device)].cpu().numpy() \
-                            if self.stats else None
+                        ncol = max(1, int(nt.max()))
+                        if ev is not None:
+                            host = _rows_after(ev, side, sess.hist, fin, ncol).numpy()
+                            acc = _rows_after(ev, side, sess.stats_acc, fin).numpy() if self.stats else None
+                        else:
+                            host = sess.hist[torch.as_tensor(fin, device=sess.hist.device), :ncol].cpu().numpy()
+                            acc = sess.stats_acc[torch.as_tensor(fin, device=sess.hist.device)].cpu().numpy() \
+                                if self.stats else None
                         for j, s in enumerate(fin.tolist()):
                             m = int(slot_msg[s])
                             tokens[m] = host[j, : int(nt[j])].tolist()
@@ -149,11 +203,12 @@ class SlotEncoder:
                         admit_blocked = False
                         live = slot_msg >= 0
                     # ---- stalls (the reference loops forever on a stream that fixes no bit)
-                    pos = f["bit_pos"]
+                    pos = f["bit_pos"] if f is not None else last_pos
+                    ntok = f["ntokens"] if f is not None else np.zeros(sess.B, dtype=np.int64)
                     moved = live & (pos != last_pos)
                     last_pos[moved], last_move[moved] = pos[moved], t
                     stuck = np.nonzero(live & (((t - last_move) >= self.stall_steps) |
-                                               (f["ntokens"] >= self.hard_cap)))[0]
+                                               (ntok >= self.hard_cap)))[0]
                     if stuck.size:
                         ids = slot_msg[stuck].tolist()[:8]
                         if all(pos[s] >= len(self.bits[slot_msg[s]]) for s in stuck):
@@ -181,7 +236,11 @@ class SlotEncoder:
                             break
                         raise KVCapacityError("no device memory for even one stream's first KV page")
                     # ---- compaction: the queue is drained and at most half the slots are live
+                    compacted = False
                     if self.allow_compact and not queue and nlive <= sess.B // 2 and sess.B > 1:
+                        compacted = True
+                        if f is not None:
+                            ntok = ntok[np.nonzero(live)[0]]
                         keep = np.nonzero(live)[0]
                         sess, logits, slot_msg, last_pos, last_move = self._compact(
                             sess, logits, keep, slot_msg, last_pos, last_move, stop)
@@ -194,11 +253,14 @@ class SlotEncoder:
                     self._map_pages(sess, slot_msg, queue, live, T0)
                     if (slot_msg >= 0).sum() < nlive:
                         admit_blocked = True
-                    # ---- token history for the next steps
-                    if int(f["ntokens"].max(initial=0)) + self.check_every + 1 > sess.hist.shape[1]:
-                        sess.ensure_history(self.check_every + 1)
+                    # ---- token history for the next steps (two periods ahead of a pipelined state copy)
+                    ahead = (2 if pipelined else 1) * self.check_every + 1
+                    if int(ntok.max(initial=0)) + ahead > sess.hist.shape[1]:
+                        sess.ensure_history(ahead)
                     if stop is not None:
                         stop.sess = sess
+                    if pipelined:
+                        pending = pin.take(sess.state)
                 key = _layout_key(logits, sess.state, sess.hist, sess.payload, lm.kv.table, lm.kv.lens,
                                   sess.stats_acc) + (lm.kv.version,)
                 if self.use_graph:
@@ -216,6 +278,8 @@ class SlotEncoder:
                 lm.advance(1)
                 t += 1
         finally:
+            if graph is not None:  # a pipelined loop ends with steps still queued on its graph
+                torch.cuda.current_stream().synchronize()
             lm.done_flags = None
             del graph
         self.sess = sess
@@ -237,7 +301,7 @@ class SlotEncoder:
 
     def _map_pages(self, sess, slot_msg, queue, live, T0):
         """Pages for every live slot's next ``check_every + 1`` positions; on a full device evict the youngest live
-        messages (fewest tokens) back to the queue's front until the others are served."""
+        messages (fewest positions fed) back to the queue's front until the others are served."""
         lm = self.lm
         while True:
             sl = np.nonzero(slot_msg >= 0)[0]
@@ -250,8 +314,7 @@ class SlotEncoder:
                 raise KVCapacityError(
                     f"message {int(slot_msg[sl[0]])} needs more KV pages than the device holds "
                     f"({lm.pool.total} pages of {lm.pool.page_bytes} B)")
-            nt = _state_fields(sess.state)["ntokens"]
-            victim = np.asarray([sl[np.argmin(nt[sl])]])
+            victim = np.asarray([sl[np.argmin(lm.kv.lens_host[sl])]])  # the youngest: fewest positions fed
             queue.appendleft(int(slot_msg[victim[0]]))
             lm.kv.release(victim)
             sess.park_slots(victim)
@@ -336,20 +399,39 @@ class SlotDecoder:
             lm.step_static(tok)
 
         t = 0
+        # check pipeline as in the encoder: a slot counts as finished once the event recorded at the previous check
+        # has passed with its last token fed (its message and positions as of that check); its bits are gathered on a
+        # side stream while the steps enqueued since run
+        pipelined = self.use_graph
+        side = torch.cuda.Stream() if pipelined else None
+        pending = None
         try:
             while True:
                 if t % self.check_every == 0:
                     live = slot_msg >= 0
-                    done = live & ((lm.kv.lens_host - T0) >= nlen_host)
+                    if pipelined:
+                        if pending is not None:
+                            ev, msg_then, fed_then = pending
+                            ev.synchronize()
+                            done = live & (slot_msg == msg_then) & (fed_then >= nlen_host)
+                        else:
+                            ev, done = None, np.zeros(slot_msg.shape, dtype=bool)
+                    else:
+                        ev, done = None, live & ((lm.kv.lens_host - T0) >= nlen_host)
                     fin = np.nonzero(done)[0]
                     if fin.size:
-                        f = _state_fields(st["state"])
-                        bad = fin[(f["flags"][fin] & L.NS_ST_ERR_DIVERGE) != 0]
+                        if ev is not None:
+                            srows = _rows_after(ev, side, st["state"], fin).numpy()
+                            f = _state_fields(torch.from_numpy(srows))
+                            rows = _rows_after(ev, side, st["out_bits"], fin)
+                        else:
+                            f = _state_fields(st["state"][torch.as_tensor(fin, device=dev)])
+                            rows = st["out_bits"][torch.as_tensor(fin, device=dev)]
+                        bad = fin[(f["flags"] & L.NS_ST_ERR_DIVERGE) != 0]
                         if bad.size:
                             raise DecodeDivergenceError(
                                 f"streams {slot_msg[bad].tolist()[:8]}: received token outside the kept top-k")
-                        rows = st["out_bits"][torch.as_tensor(fin, device=dev)]
-                        got = _bit_rows_to_lists(rows, f["bit_pos"][fin])
+                        got = _bit_rows_to_lists(rows, f["bit_pos"])
                         for j, s in enumerate(fin.tolist()):
                             out[int(slot_msg[s])] = got[j]
                         lm.kv.release(fin)
@@ -405,6 +487,10 @@ class SlotDecoder:
                         slot_msg, nlen_host = slot_msg[keep].copy(), nlen_host[keep].copy()
                         self.compactions += 1
                     lm.stop_len = st["stop"] if getattr(self.p, "skip_done", True) else None
+                    if pipelined:
+                        ev_now = torch.cuda.Event()
+                        ev_now.record()
+                        pending = (ev_now, slot_msg.copy(), lm.kv.lens_host - T0)
                 key = _layout_key(logits, st["state"], st["tokmat"], lm.kv.table, lm.kv.lens) + (lm.kv.version,)
                 if self.use_graph:
                     if graph is None or key != gkey:
@@ -419,6 +505,8 @@ class SlotDecoder:
                 lm.advance(1)
                 t += 1
         finally:
+            if graph is not None:
+                torch.cuda.current_stream().synchronize()
             lm.stop_len = None
             del graph
         return out
