@@ -1,10 +1,9 @@
-#!/bin/bash
-# Small-batch A/B of the two single-pass coder forms (one wave per stream vs the split workgroup-per-stream form):
-# tools/split_ab.sh OUTDIR "phase_timing args" B1 B2 ...   (each run under its own time limit; stops at a failure)
 set -e
-out=$1; args=$2; shift 2
-mkdir -p "$out"
-for b in "$@"; do
-    NSG_SPLIT_MAX_B=0 timeout -k 10 120 python tools/phase_timing.py --batch "$b" $args > "$out/wave_b$b.jsonl" 2>&1
-    NSG_SPLIT_MAX_B=1000000 timeout -k 10 120 python tools/phase_timing.py --batch "$b" $args > "$out/split_b$b.jsonl" 2>&1
+mkdir -p gpurun_out/r06l
+for v in base rows128 rows64; do
+  if [ $v = base ]; then unset NSG_CODER_LIB; else export NSG_CODER_LIB=neuralsteganography_amd/_build/variants/$v.so; fi
+  for args in "--B 1 --L 544" "--B 1 --L 160" "--B 1 --L 1000" "--B 4096 --L 544" "--B 4096 --L 160" "--B 4096 --L 900" "--B 4096 --L 544 --kv fp8 --window 256"; do
+    echo -n "$v $args " >> gpurun_out/r06l/split.txt
+    timeout -k 10 120 python tools/paged_attn_probe.py $args --only c --steps 50 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['kernel_ms']*1000,2), 'us', round(d['GBps']))" >> gpurun_out/r06l/split.txt
+  done
 done
