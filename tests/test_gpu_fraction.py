@@ -243,8 +243,8 @@ def test_fraction_scratch_budget_splits_a_group_instead_of_failing_it(F, monkeyp
     that do (each fits alone), so every message still gets the restatement's tokens -- a message never fails because
     of what else is in its batch."""
     rng = np.random.default_rng(12)
-    streams = [[(lambda p: p / p.sum())(rng.random(300)) for _ in range(30)] for _ in range(6)]
-    payloads = [bytes([b, 7]) for b in range(6)]
+    streams = [[(lambda p: p / p.sum())(rng.random(300)) for _ in range(12)] for _ in range(6)]
+    payloads = [bytes([b]) for b in range(6)]  # every message encodes in the restatement (checked on the CPU)
     dv = F._Device(1, F.DEFAULT_CAP_LIMBS)
     one = int(dv.L.ns_frac_scratch_bytes(dv.ctx, 1, 300, 16, 8 * F.DEFAULT_TABLE_LIMBS))
     dv.close()
@@ -257,7 +257,7 @@ def test_fraction_scratch_budget_splits_a_group_instead_of_failing_it(F, monkeyp
             assert isinstance(g, Exception) and _kind(g) == want, (b, g, want)
         else:
             assert g == want[0], b
-    assert sum(not isinstance(g, Exception) for g in got) >= 3
+    assert all(not isinstance(g, Exception) for g in got)  # before: all six failed with FractionCapacityError
 
 
 def test_fraction_capacity_is_per_message(F):
