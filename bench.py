@@ -593,7 +593,8 @@ def measured_traffic(args, version):
         except (OSError, ValueError):
             continue
         if (rec.get("library_version") == version and rec.get("batch") == args.batch and rec.get("vocab") == args.vocab
-                and rec.get("dtype") == args.dtype and rec.get("topk") == args.topk):
+                and rec.get("dtype") == args.dtype and rec.get("topk") == args.topk
+                and rec.get("kernel", "coder_step_kernel") == "coder_step_kernel"):
             best = (rec["traffic_bytes_per_launch"], "from " + str(Path(path).relative_to(ROOT)) +
                     " (committed rocprofv3 PMC record of this library build; not measured in this run)")
     return best

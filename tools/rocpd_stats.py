@@ -20,9 +20,22 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--window-from", default=None, help="kernel name substring; the window starts at its n-th launch")
     ap.add_argument("--nth", type=int, default=1, help="which launch of --window-from opens the window (1-based)")
+    ap.add_argument("--after-fill-run", type=int, default=0,
+                    help="the window starts after the last run of at least this many consecutive torch elementwise "
+                         "kernels (tools/c3_job_probe.py: the page pool's warm-up fill just before the job)")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     rows = con.execute("select name, start, end, duration from kernels order by start").fetchall()
+    if a.after_fill_run:
+        last, i = 0, 0
+        while i < len(rows):
+            j = i
+            while j < len(rows) and "vectorized_elementwise" in rows[j][0]:
+                j += 1
+            if j - i >= a.after_fill_run:
+                last = j
+            i = max(j, i + 1)
+        rows = rows[last:]
     if a.window_from:
         hits = [i for i, r in enumerate(rows) if a.window_from in r[0]]
         if len(hits) < a.nth:
