@@ -22,6 +22,7 @@ under torch.distributed.run.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -486,7 +487,9 @@ def end_to_end(args, rank, world, dev, kv_dtype="fp16", window=0, batch=None, mo
                             f"from a 32-token context, "
                             + (f"head scaled x{logit_scale} (trained-entropy rows), " if logit_scale != 1.0 else "")
                             + (f"attention window {window} (opt-in)" if window else "unbounded KV cache")})
+    lm.lm.release_cache()
     del lm
+    gc.collect()
     torch.cuda.empty_cache()
     return out
 
@@ -543,7 +546,9 @@ def c5_guard(args, rank, world, dev, n=1024, max_bytes=256):
     rev_s = time.perf_counter() - t1
     npass_all, n_all, gen_max, _ = reduce_job(len(passed), n, gen_s, 0.0, device=dev)
     ex_all, _, rev_max, _ = reduce_job(exact, 0, rev_s, 0.0, device=dev)
+    lm.lm.release_cache()
     del lm
+    gc.collect()
     torch.cuda.empty_cache()
     return {"secrets": int(n_all), "secret_bytes": f"0..{max_bytes - 1}", "gate": gate, "seconds": gen_max,
             "covers_per_s": npass_all / gen_max, "secrets_per_s": n_all / gen_max,

@@ -26,6 +26,7 @@ Hugging Face ``GPT2LMHeadModel`` (pretrained when available offline, random-init
 from __future__ import annotations
 
 import math
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -498,8 +499,14 @@ class BatchedGPT2:
             seg = self.kv_segment_pages
             if seg is None:
                 seg = min(1024, max(64, 1 << max(0, 2 * int(B or self.B or 1) - 1).bit_length()))
+            me = weakref.ref(self)  # no reference cycle: a dropped model frees its pool at once (no gc pass needed)
+
+            def budget():
+                lm = me()
+                return lm._pool_budget() if lm is not None else 0
+
             self.pool = KVPagePool(s.n_layer, s.n_head, s.n_embd // s.n_head, self.kv_torch_dtype, self.device,
-                                   budget_bytes=self._pool_budget, seg_pages=seg)
+                                   budget_bytes=budget, seg_pages=seg)
         return self.pool
 
     def begin_slots(self, B: int, T0: int, max_new: int = 32) -> None:
