@@ -521,16 +521,23 @@ class HipArithmeticLM:
             return bits, [cn[: min(n, len(token_lists[i])), i].tolist() for i in range(B)]
 
         t = 0
+        lens = np.asarray([len(tl) for tl in token_lists])
         while t < sess.T:
             sess.step(logits)
             counts[t].copy_(sess.state[:, 2])  # bit_pos after token t
             t += 1
             if t < sess.T:
-                logits = self.lm.step(sess.tok[t - 1])
+                logits = self._lm_step(sess.tok[t - 1], lens > t)  # streams with a token t left to decode
             if done is not None and t % check_every == 0 and t < sess.T and done(*snapshot(t)):
                 break
         return snapshot(t)
 
+
+    def _lm_step(self, tokens, live):
+        """``lm.step`` for the lockstep decodes, telling a native model which streams still need logits."""
+        if getattr(self.lm, "native", False):
+            return self.lm.step(tokens, live=live)
+        return self.lm.step(tokens)
 
     def decode_tokens_repair(self, token_lists: Sequence[Sequence[int]], context: Sequence[int], *,
                              quality: Mapping[str, object], enc=None) -> List[List[int]]:
@@ -616,7 +623,8 @@ class HipArithmeticLM:
                 break
             if done is not None and steps % check_every == 0 and done(sess.bits(), counts, lists):
                 break
-            logits = self.lm.step(torch.tensor(feed, device=self.device, dtype=torch.long))
+            nxt = [pos[b] < len(lists[b]) and not dead[b] for b in range(B)]  # streams that decode a next token
+            logits = self._lm_step(torch.tensor(feed, device=self.device, dtype=torch.long), nxt)
         return sess.bits(), counts, lists, edits
 
     def sample_batch(self, B: int, length: int, context: Sequence[int], *, temperature: float = 1.0,

@@ -660,18 +660,33 @@ class BatchedGPT2:
         return self._static_logits
 
     @torch.no_grad()
-    def step(self, tokens: torch.Tensor) -> torch.Tensor:
-        """Feed one token per stream (``[B]`` int); position = cache length mod n_positions."""
+    def step(self, tokens: torch.Tensor, live=None) -> torch.Tensor:
+        """Feed one token per stream (``[B]`` int); position = cache length mod n_positions.  ``live`` (host bool
+        ``[B]``, native path): only these streams get pages and attention this step -- a lockstep caller whose
+        streams end at different lengths (the span splitter's decodes) stops paying, in memory and reads, for the
+        finished ones; their logits rows are not meaningful afterwards."""
         B = self.B
         if tokens.shape != (B,):
             raise ValueError(f"expected {B} tokens")
         if self.native:
-            if not self.reserve(1):
-                from ..exceptions import KVCapacityError
+            from ..exceptions import KVCapacityError
 
+            if live is None:
+                ok = self.reserve(1)
+            else:
+                live = np.asarray(live, dtype=bool).reshape(B)
+                ok = self.kv.ensure(np.nonzero(live)[0], self.L + 1).size == 0
+            if not ok:
                 raise KVCapacityError(f"KV cache full at {self.L} positions for B={B}: no device memory for a page")
             out = torch.empty((B, self.ld), device=self.device, dtype=self.logits_dtype)
-            self._decode_native(tokens, out)
+            saved = self.stop_len
+            if live is not None and not live.all():  # the attention skips a stream whose length reached its stop
+                stop = np.where(live, np.iinfo(np.int32).max, 0).astype(np.int32)
+                self.stop_len = torch.from_numpy(stop).to(self.device)
+            try:
+                self._decode_native(tokens, out)
+            finally:
+                self.stop_len = saved
             self.advance(1)
             return out
         if self.L >= self.max_len:

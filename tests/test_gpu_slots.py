@@ -252,3 +252,22 @@ def test_device_string_cuda_round_trip():
         toks = lm.encode_batch(bits, synthetic.DEFAULT_CONTEXT, quality=Q, graphs=graphs)
         out = lm.decode_batch(toks, synthetic.DEFAULT_CONTEXT, quality=Q, graphs=graphs)
         assert all(o[: len(b)] == b for o, b in zip(out, bits))
+
+
+def test_slots_keep_statistics_finish_sent_and_stop_text():
+    """Refilled slots carry every per-message feature of the lockstep batch: the statistics accumulators (reset per
+    message), the finish_sent tail and the '<eos>'-style stop text (the eager, per-step checked loop) -- the same
+    tokens and statistics through 3-4 slots as all at once."""
+    lm = _provider(scale=4.0, seed=47)
+    ctx = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(200 + s, n)) for s, n in
+            enumerate([6, 1, 12, 3, 9, 2, 7, 5, 10, 4])]
+    qf = dict(Q, finish_sent=True)
+    a, sa = lm.encode_batch(bits, ctx, quality=qf, return_stats=True)
+    b, sb = lm.encode_batch(bits, ctx, quality=qf, return_stats=True, slots=3)
+    assert a == b
+    assert sa == sb  # per-message float64 accumulators, reset when a slot takes a message
+    c = lm.encode_batch(bits, ctx, quality=Q, stop_text=".", slots=4)
+    d = lm.encode_batch(bits, ctx, quality=Q, stop_text=".")
+    assert c == d
+    assert any(lm.tokenizer.decode(t).endswith(".") for t in d)
