@@ -124,7 +124,8 @@ class SlotEncoder:
 
         lm, S, N = self.lm, self.S, self.N
         max_bits = max(len(b) for b in self.bits)
-        budget = 2 * max_bits + 64
+        # initial token-history / page-table width (both grow on demand; a provider may set a small one in tests)
+        budget = getattr(self.p, "slot_budget_tokens", None) or 2 * max_bits + 64
         logits = lm.prefill(self.context, S, budget)  # [S, ld]: every slot starts on the context's logits
         first = lm.first_logits
         T0 = lm.kv.T0

@@ -254,20 +254,38 @@ def test_device_string_cuda_round_trip():
         assert all(o[: len(b)] == b for o, b in zip(out, bits))
 
 
-def test_slots_keep_statistics_finish_sent_and_stop_text():
-    """Refilled slots carry every per-message feature of the lockstep batch: the statistics accumulators (reset per
-    message), the finish_sent tail and the '<eos>'-style stop text (the eager, per-step checked loop) -- the same
-    tokens and statistics through 3-4 slots as all at once."""
+def test_slots_keep_statistics_and_stop_text():
+    """Refilled slots carry the per-message features of the lockstep batch: the statistics accumulators (reset per
+    message) and the '<eos>'-style stop text (the eager, per-step checked loop) -- the same tokens and statistics
+    through 3-4 slots as all at once."""
     lm = _provider(scale=4.0, seed=47)
     ctx = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(200 + s, n)) for s, n in
-            enumerate([6, 1, 12, 3, 9, 2, 7, 5, 10, 4])]
-    qf = dict(Q, finish_sent=True)
-    a, sa = lm.encode_batch(bits, ctx, quality=qf, return_stats=True)
-    b, sb = lm.encode_batch(bits, ctx, quality=qf, return_stats=True, slots=3)
+            enumerate([40, 10, 90, 30, 70, 20, 60, 50, 80, 35])]
+    a, sa = lm.encode_batch(bits, ctx, quality=Q, return_stats=True)
+    b, sb = lm.encode_batch(bits, ctx, quality=Q, return_stats=True, slots=3)
     assert a == b
     assert sa == sb  # per-message float64 accumulators, reset when a slot takes a message
-    c = lm.encode_batch(bits, ctx, quality=Q, stop_text=".", slots=4)
-    d = lm.encode_batch(bits, ctx, quality=Q, stop_text=".")
+    c = lm.encode_batch(bits, ctx, quality=Q, stop_text="e", slots=4)
+    d = lm.encode_batch(bits, ctx, quality=Q, stop_text="e")
     assert c == d
-    assert any(lm.tokenizer.decode(t).endswith(".") for t in d)
+    stopped = [i for i, t in enumerate(d) if len(t) < len(a[i])]
+    assert stopped, "no cover reached the stop text: pick another one"
+    for i in stopped:
+        assert lm.tokenizer.decode(d[i]).endswith("e") and d[i] == a[i][: len(d[i])]
+
+
+def test_history_and_table_growth_inside_the_pipelined_loop():
+    """A tiny initial token history and page-table width (8 tokens) make the pipelined loop grow both several times
+    (each a re-captured graph): the tokens equal the eager loop's and the default budget's."""
+    lm = _provider(seed=48)
+    ctx = synthetic.DEFAULT_CONTEXT
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(300 + s, n)) for s, n in enumerate([20, 5, 30, 12])]
+    ref = lm.encode_batch(bits, ctx, quality=Q)
+    lm.slot_budget_tokens = 8
+    try:
+        assert lm.encode_batch(bits, ctx, quality=Q) == ref
+        assert lm.encode_batch(bits, ctx, quality=Q, graphs=False, slots=2) == ref
+    finally:
+        lm.slot_budget_tokens = None
+    assert max(map(len, ref)) > 64  # several growths of the 8-token start
