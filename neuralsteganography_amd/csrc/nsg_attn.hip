@@ -477,10 +477,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
             pL0 = a.lens[b];
             const bool skip = (a.done && (a.done[(int64_t)b * a.done_stride] & 1u)) || (a.stop && pL0 >= a.stop[b]);
             if (!skip) {
-                const int jj = pL0 - a.T0;  // the new token's stream row: its page must exist (host invariant)
-                const uint64_t pg =
-                    (jj >= 0 && (jj >> 5) < a.max_chunks) ? a.table[(int64_t)b * a.tstride + (jj >> 5)] : 0;
-                if (pg == 0 || (pg & 15u)) {
+                const int jj = pL0 - a.T0;  // the new token's stream row: inside the table (its page is checked by
+                                            // the pair's tasks, one load fewer before the streaming starts)
+                if (jj < 0 || (jj >> 5) >= a.max_chunks) {
                     pst = 2;  // no page: poison the output (NaN logits the coder rejects), never write
                 } else {
                     pst = 1;
@@ -539,11 +538,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         auto kaddr = [&](uint64_t page, int jj) -> E* { return (E*)page + hoff + (int64_t)(jj & 31) * ATT_D; };
         const E* kpb = (const E*)a.kp + (int64_t)h * a.ph + c * DPL;
         const E* vpb = (const E*)a.vp + (int64_t)h * a.ph + c * DPL;
-        if (g == 0 && wv == 0) {  // KV append of the new token (position L0, page checked above)
-            E* kd = kaddr(trow[(L0 - T0) >> 5], L0 - T0);
-            *(Raw*)kd = knew;
-            *(Raw*)(kd + a.v_off) = vnew;
-        }
         float m = -1e30f, l = 0.0f;
         float acc[DPL];
 #pragma unroll
@@ -570,6 +564,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
             pa = readlane64(pgA, k - kbase);
             pb = readlane64(pgB, k - kbase);
         };
+        // the new token's page: a missing one (host invariant broken) poisons the pair -- every one of its tasks
+        // reads the same entry, writes nothing and hands NaN on (S = 1: the output row; S > 1: the partials, which
+        // the merge turns into NaN).  The first iterations' page addresses are requested before it, so both table
+        // reads are in flight together (the prefetch reads entries of cached rows only: inside the table).
+        {
+            uint64_t pa0, pb0;
+            pages_of(0, pa0, pb0);
+        }
+        const uint64_t apage = trow[(L0 - T0) >> 5];
+        const bool bad = apage == 0 || (apage & 15u);
+        const int Lend = bad ? 0 : Lk;  // the streaming loops run while j0 < Lend
+        if (g == 0 && wv == 0 && !bad) {  // KV append of the new token (position L0)
+            E* kd = kaddr(apage, L0 - T0);
+            *(Raw*)kd = knew;
+            *(Raw*)(kd + a.v_off) = vnew;
+        }
         // one iteration = RPI*NI = 32 consecutive rows from j0; GENERAL handles the prefix boundary, the clamp past
         // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages
         auto load_chunk = [&](int j0, int k, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         Raw kr[NI], vr[NI];
         if constexpr (P > 1) {
             int k = 0;
-            for (int j0 = jbeg; j0 < Lk; j0 += step, ++k) {
+            for (int j0 = jbeg; j0 < Lend; j0 += step, ++k) {
                 if (interior(j0)) {
                     load_chunk(j0, k, std::false_type{}, kr, vr);
                     math_chunk(j0, std::false_type{}, kr, vr);
@@ -653,15 +663,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         } else {  // one pair per workgroup (small batches): register double buffer, as the lockstep kernel
             Raw kn[NI], vn[NI];
             int j0 = jbeg, k = 0;
-            if (j0 < Lk) {
+            if (j0 < Lend) {
                 if (interior(j0))
                     load_chunk(j0, 0, std::false_type{}, kr, vr);
                 else
                     load_chunk(j0, 0, std::true_type{}, kr, vr);
             }
-            for (; j0 < Lk; j0 += step, ++k) {
+            for (; j0 < Lend; j0 += step, ++k) {
                 const int j1 = j0 + step;
-                if (j1 < Lk) {
+                if (j1 < Lend) {
                     if (interior(j1))
                         load_chunk(j1, k + 1, std::false_type{}, kn, vn);
                     else
@@ -691,6 +701,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
                 acc[d] = acc[d] * fa + ao * fo;
             }
             m = mn;
+        }
+        if (bad) {
+            m = l = __builtin_nanf("");
+#pragma unroll
+            for (int d = 0; d < DPL; ++d) acc[d] = __builtin_nanf("");
         }
         if (S == 1) {  // the whole pair in this wave: out = acc / l, as the lockstep kernel (a 1-way merge is exact)
             if (g == 0) {
