@@ -131,6 +131,12 @@ class BatchedGPT2:
         # optional per-stream stop positions (int32 [B]): a stream whose cache length reached its stop skips its
         # attention (decode: the position after which its logits are no longer read)
         self.stop_len = None
+        # decode-step lanes (native path): 2 = the batch's two row halves on two streams with alternating attention
+        # launches (one half's GEMMs overlap the other's attention); 1 = one launch chain
+        self.decode_lanes = 1
+        self.decode_lanes_min_batch = 1024
+        self.decode_lanes_order = "alternate"  # or "free": no ordering between the lanes
+        self._side = None
         if self.native:
             from .. import _lib
 
@@ -558,29 +564,13 @@ class BatchedGPT2:
         from .. import _lib
         from ..coder import _stream_handle
 
-        s = self.shape
         kv = self.kv
-        B, C = kv.B, s.n_embd
-        H, D = s.n_head, C // s.n_head
+        B = kv.B
         L = _lib.lib()
         st = _stream_handle()
-        nb = self._native_buffers(B)
-        h, a, qkv, o, f = nb["h"], nb["a"], nb["qkv"], nb["o"], nb["f"]
         tok = tokens if tokens.dtype == torch.int32 else tokens.to(torch.int32)
         if not tok.is_contiguous() or tok.shape != (B,):
             tok = tok.reshape(B).contiguous()
-        T0 = kv.T0
-        eps = float(s.eps)
-
-        def ok(rc, what):
-            if rc != 0:
-                raise RuntimeError(f"{what} failed ({rc})")
-
-        def gemm(x, wt, bias, y, epi, N, K):
-            ok(L.ns_lm_gemm(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0),
-                            bias.data_ptr() if bias is not None else None, y.data_ptr(), y.stride(0), B, N, K, epi,
-                            st), "ns_lm_gemm")
-
         df = self.done_flags
         if df is not None and (df.dtype != torch.int32 or df.shape != (B,) or not _same_device(df.device, self.device)):
             raise ValueError(f"done_flags must be an int32 [{B}] view on {self.device}")
@@ -592,39 +582,124 @@ class BatchedGPT2:
         stop_ptr = sl.data_ptr() if sl is not None else None
         if out.shape != (B, self.ld) or out.stride(1) != 1:
             raise ValueError(f"logits buffer must be [{B}, {self.ld}]")
-        lens = kv.lens.data_ptr()
+        lanes = self._lanes(B)
+        if len(lanes) == 1:
+            self._decode_rows(L, st, tok, out, 0, B, done_ptr, done_stride, stop_ptr)
+            return out
+        # two lanes (row halves) on two streams, their attention launches alternating (lane 0 layer i, lane 1 layer
+        # i, lane 0 layer i + 1, ...): one lane's GEMMs / layer norms run beside the other lane's HBM-bound attention
+        # instead of after it.  Rows are independent (batch invariance), so the bits are those of one launch chain.
+        side = self._side_stream()
+        main = torch.cuda.current_stream(self.device)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        side.wait_event(fork)
+        (r0, n0), (r1, n1) = lanes
+        steps = [self._decode_rows(L, st, tok, out, r0, n0, done_ptr, done_stride, stop_ptr, gen=True),
+                 self._decode_rows(L, side.cuda_stream, tok, out, r1, n1, done_ptr, done_stride, stop_ptr, gen=True)]
+        streams = (main, side)
+        alternate = self.decode_lanes_order == "alternate"
+        prev = None  # (lane, event after its latest attention launch)
+        for _ in range(self.shape.n_layer):
+            for k in (0, 1):
+                next(steps[k])  # up to the attention launch
+                if alternate and prev is not None:
+                    streams[k].wait_event(prev[1])
+                next(steps[k])  # the attention launch
+                if alternate:
+                    ev = torch.cuda.Event()
+                    ev.record(streams[k])
+                    prev = (k, ev)
+        for k in (0, 1):
+            for _ in steps[k]:  # ln_f and the head
+                pass
+        join = torch.cuda.Event()
+        join.record(side)
+        main.wait_event(join)
+        return out
+
+    def _lanes(self, B: int):
+        """Row ranges of the decode step's lanes: one, or two halves (``decode_lanes`` = 2) when B is large enough
+        for both halves to fill the chip."""
+        if self.decode_lanes <= 1 or B < self.decode_lanes_min_batch:
+            return [(0, B)]
+        h = (B // 2 + 15) // 16 * 16
+        return [(0, h), (h, B - h)]
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
+    def _decode_rows(self, L, st, tok, out, r0, n, done_ptr, done_stride, stop_ptr, gen=False):
+        """The decode step's launches for rows [r0, r0 + n) on stream ``st``.  ``gen``: a generator that yields
+        before and after each layer's attention launch (the caller orders the lanes' attention launches)."""
+        it = self._decode_rows_gen(L, st, tok, out, r0, n, done_ptr, done_stride, stop_ptr)
+        if gen:
+            return it
+        for _ in it:
+            pass
+
+    def _decode_rows_gen(self, L, st, tok, out, r0, B, done_ptr, done_stride, stop_ptr):
+        from .. import _lib
+
+        s = self.shape
+        kv = self.kv
+        C = s.n_embd
+        H, D = s.n_head, C // s.n_head
+        nb = self._native_buffers(kv.B)
+
+        def row(t, r=r0):  # address of row r of a [*, ...] tensor
+            return t.data_ptr() + r * t.stride(0) * t.element_size()
+
+        h, a, qkv, o, f = (row(nb[k]) for k in ("h", "a", "qkv", "o", "f"))
+        ldq, ldf = nb["qkv"].stride(0), nb["f"].stride(0)
+        T0 = kv.T0
+        eps = float(s.eps)
+
+        def ok(rc, what):
+            if rc != 0:
+                raise RuntimeError(f"{what} failed ({rc})")
+
+        def gemm(x, ldx, wt, bias, y, ldy, epi, N, K):
+            ok(L.ns_lm_gemm(x, ldx, wt.data_ptr(), wt.stride(0), bias.data_ptr() if bias is not None else None, y,
+                            ldy, B, N, K, epi, st), "ns_lm_gemm")
+
+        lens = row(kv.lens)
         lw0 = self.layers[0]
-        ok(L.ns_lm_embed_ln_rows(tok.data_ptr(), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
-                                 lens, h.data_ptr(), C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(),
-                                 a.data_ptr(), C, B, C, eps, st), "ns_lm_embed_ln_rows")
+        ok(L.ns_lm_embed_ln_rows(row(tok), self.wte.data_ptr(), self.wpe.data_ptr(), s.vocab, s.n_positions,
+                                 lens, h, C, lw0["ln1_w"].data_ptr(), lw0["ln1_b"].data_ptr(), a, C, B, C, eps, st),
+           "ns_lm_embed_ln_rows")
 
-        def ln_gemm(ln_w, ln_b, wt, bias, y, epi, N):  # ln(h) -> GEMM, one launch at small B (same bits)
-            ok(L.ns_lm_ln_gemm(h.data_ptr(), C, ln_w.data_ptr(), ln_b.data_ptr(), eps, wt.data_ptr(), wt.stride(0),
-                               bias.data_ptr(), y.data_ptr(), y.stride(0), B, N, C, epi, a.data_ptr(), C, st),
-               "ns_lm_ln_gemm")
+        def ln_gemm(ln_w, ln_b, wt, bias, y, ldy, epi, N):  # ln(h) -> GEMM, one launch at small B (same bits)
+            ok(L.ns_lm_ln_gemm(h, C, ln_w.data_ptr(), ln_b.data_ptr(), eps, wt.data_ptr(), wt.stride(0),
+                               bias.data_ptr(), y, ldy, B, N, C, epi, a, C, st), "ns_lm_ln_gemm")
 
+        table = row(kv.table)
+        done = done_ptr + r0 * done_stride * 4 if done_ptr else None
+        stop = stop_ptr + r0 * 4 if stop_ptr else None
         for i, lw in enumerate(self.layers):
             if i > 0:
-                ln_gemm(lw["ln1_w"], lw["ln1_b"], lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C)
+                ln_gemm(lw["ln1_w"], lw["ln1_b"], lw["qkv_wt"], lw["qkv_b"], qkv, ldq, _lib.NS_LM_EPI_STORE, 3 * C)
             else:  # ln_1 of layer 0 comes with the embedding
-                gemm(a, lw["qkv_wt"], lw["qkv_b"], qkv, _lib.NS_LM_EPI_STORE, 3 * C, C)
+                gemm(a, C, lw["qkv_wt"], lw["qkv_b"], qkv, ldq, _lib.NS_LM_EPI_STORE, 3 * C, C)
             kp = self.kp[i, 0] if T0 else None  # [H, T0, D]
             vp = self.vp[i, 0] if T0 else None
-            rc = L.ns_decode_attention_paged(qkv.data_ptr(), qkv.stride(0), kv.table.data_ptr(), kv.table.stride(0),
-                                             kv.width, kv.pool.layer_offset(i), kp.data_ptr() if T0 else None,
-                                             vp.data_ptr() if T0 else None, kp.stride(0) if T0 else 0, T0, B, H, D,
-                                             lens, self.window, self._kv_format, done_ptr, done_stride, stop_ptr,
-                                             o.data_ptr(), o.stride(0), 1.0 / math.sqrt(D), st)
+            yield  # before the attention launch
+            rc = L.ns_decode_attention_paged(qkv, ldq, table, kv.table.stride(0), kv.width, kv.pool.layer_offset(i),
+                                             kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
+                                             kp.stride(0) if T0 else 0, T0, B, H, D, lens, self.window,
+                                             self._kv_format, done, done_stride, stop, o, C, 1.0 / math.sqrt(D), st)
             ok(rc, "ns_decode_attention_paged")
-            gemm(o, lw["o_wt"], lw["o_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, C)
-            ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, _lib.NS_LM_EPI_GELU, 4 * C)
-            gemm(f, lw["pr_wt"], lw["pr_b"], h, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
+            yield  # after it
+            gemm(o, C, lw["o_wt"], lw["o_b"], h, C, _lib.NS_LM_EPI_RESIDUAL, C, C)
+            ln_gemm(lw["ln2_w"], lw["ln2_b"], lw["fc_wt"], lw["fc_b"], f, ldf, _lib.NS_LM_EPI_GELU, 4 * C)
+            gemm(f, ldf, lw["pr_wt"], lw["pr_b"], h, C, _lib.NS_LM_EPI_RESIDUAL, C, 4 * C)
         # ln_f also advances every stream's cache length (no launch of its own)
-        ok(L.ns_lm_layernorm_rows(h.data_ptr(), C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a.data_ptr(), C, B,
-                                  C, eps, lens, st), "ns_lm_layernorm_rows")
+        ok(L.ns_lm_layernorm_rows(h, C, self.lnf_w.data_ptr(), self.lnf_b.data_ptr(), a, C, B, C, eps, lens, st),
+           "ns_lm_layernorm_rows")
         epi = _lib.NS_LM_EPI_STORE_F32 if out.dtype == torch.float32 else _lib.NS_LM_EPI_STORE
-        gemm(a, self.head_t, None, out, epi, self.ld, C)
-        return out
+        gemm(a, C, self.head_t, None, row(out), out.stride(0), epi, self.ld, C)
 
     # ------------------------------------------------------------------ graph-capturable decode step
     def begin_static(self, logits_out: torch.Tensor) -> None:

@@ -289,3 +289,24 @@ def test_history_and_table_growth_inside_the_pipelined_loop():
     finally:
         lm.slot_budget_tokens = None
     assert max(map(len, ref)) > 64  # several growths of the 8-token start
+
+
+@pytest.mark.parametrize("order", ["alternate", "free"])
+def test_two_decode_lanes_give_the_same_tokens(order):
+    """The decode step as two row halves on two streams (``decode_lanes = 2``, one half's GEMMs beside the other's
+    attention): the same tokens as one launch chain -- graph-replayed with refilled slots and compaction, eager -- and
+    the decode round-trips through the lanes too."""
+    lm = _provider(seed=49)
+    ctx = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
+    bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(400 + s, n)) for s, n in
+            enumerate([24, 3, 40, 16, 1, 31, 24, 8, 48, 12, 20, 5, 33, 9, 17, 26, 2, 44, 11, 30])]
+    ref = lm.encode_batch(bits, ctx, quality=Q)
+    lm.lm.decode_lanes, lm.lm.decode_lanes_min_batch, lm.lm.decode_lanes_order = 2, 2, order
+    try:
+        assert lm.encode_batch(bits, ctx, quality=Q) == ref
+        assert lm.encode_batch(bits, ctx, quality=Q, slots=7) == ref
+        assert lm.encode_batch(bits, ctx, quality=Q, graphs=False) == ref
+        out = lm.decode_batch(ref, ctx, quality=Q)
+        assert all(o[: len(b)] == b for o, b in zip(out, bits))
+    finally:
+        lm.lm.decode_lanes = 1

@@ -1,6 +1,6 @@
 """Host cost of one hipGraph replay of the lockstep step vs its GPU time: B streams, the captured step replayed
 64 times (host enqueue time without a sync, then wall time to completion, then HIP events on the stream).
-usage: python tools/replay_probe.py [--batch 4096] [--kv fp16] [--window 0] [--reps 64]"""
+usage: python tools/replay_probe.py [--batch 4096] [--kv fp16] [--window 0] [--reps 64] [--lanes 2 --order free]"""
 import argparse
 import json
 import os
@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--reps", type=int, default=64)
     ap.add_argument("--skip", type=int, default=300, help="replays before timing (cache length ~ mid-job)")
     ap.add_argument("--blocks", type=int, default=0, help="then this many more blocks of --reps replays, timed")
+    ap.add_argument("--lanes", type=int, default=1, help="decode-step lanes (BatchedGPT2.decode_lanes)")
+    ap.add_argument("--order", default="alternate", help="lane order: alternate | free")
+    ap.add_argument("--eager", action="store_true", help="launch every step eagerly instead of replaying the graph")
     args = ap.parse_args()
     import torch
 
@@ -29,19 +32,29 @@ def main():
     B = args.batch
     lm = A.HipArithmeticLM(random_gpt2("gpt2", seed=1234), None, logits_dtype="f16", max_batch=B, kv_dtype=args.kv,
                            attention_window=args.window)
+    lm.lm.decode_lanes, lm.lm.decode_lanes_order = args.lanes, args.order
     q = {"temp": 0.9, "precision": 26, "topk": 300}
     ctx_ids = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 1024)) for s in range(B)]
     params = A.coder_params_from_quality(q, lm.vocab, lm.logits_dtype, lm.banned)
     ctx = lm._coder(params, B)
     budget = 2 * 8192 + 64 if not args.blocks else 2 * 8192 + 64 + args.blocks * args.reps
+    lm.lm.warm_pool(B=B)
     logits = lm.lm.prefill(ctx_ids, B, budget)
+    if not lm.lm.reserve(args.skip + args.reps * (2 + args.blocks) + 8):  # the paged cache: map every page ahead
+        raise SystemExit("no device memory for the pages")
     sess = coder_mod.EncodeSession(ctx, bits, max_tokens=budget)
     g = A._StepGraph(lm.lm, lambda lg: sess.step(lg), logits)
+    if args.eager:
+        def eager():
+            g._body()
+            g.lm.L += 1
+
+        g.replay = eager
     for _ in range(args.skip):
         g.replay()
     torch.cuda.synchronize()
-    out = {"batch": B, "kv": args.kv, "window": args.window, "reps": args.reps, "L": lm.lm.L}
+    out = {"batch": B, "lanes": args.lanes, "order": args.order, "eager": args.eager, "kv": args.kv, "window": args.window, "reps": args.reps, "L": lm.lm.L}
     t0 = time.perf_counter()
     for _ in range(args.reps):
         g.replay()
