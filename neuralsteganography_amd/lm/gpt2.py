@@ -621,9 +621,11 @@ class BatchedGPT2:
     def _lanes(self, B: int):
         """Row ranges of the decode step's lanes: one, or two halves (``decode_lanes`` = 2) when B is large enough
         for both halves to fill the chip."""
-        if self.decode_lanes <= 1 or B < self.decode_lanes_min_batch:
+        if self.decode_lanes <= 1 or B < max(2, self.decode_lanes_min_batch):
             return [(0, B)]
-        h = (B // 2 + 15) // 16 * 16
+        h = (B // 2 + 15) // 16 * 16  # 16-row aligned split (whole MFMA row blocks in lane 0)
+        if not 0 < h < B:
+            h = B // 2
         return [(0, h), (h, B - h)]
 
     def _side_stream(self):
@@ -648,6 +650,8 @@ class BatchedGPT2:
         C = s.n_embd
         H, D = s.n_head, C // s.n_head
         nb = self._native_buffers(kv.B)
+        if not (B > 0 and r0 >= 0 and r0 + B <= kv.B):  # host check before any launch: rows inside every buffer
+            raise ValueError(f"decode rows [{r0}, {r0 + B}) outside the batch of {kv.B}")
 
         def row(t, r=r0):  # address of row r of a [*, ...] tensor
             return t.data_ptr() + r * t.stride(0) * t.element_size()
