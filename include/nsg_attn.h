@@ -90,7 +90,8 @@ int ns_decode_attention_ex(const void* d_qkv, int64_t qkv_stride, void* d_k_cach
                            int64_t out_stride, float scale, void* hip_stream);
 
 /* ns_decode_attention_ex over a PAGED cache with a cache length PER STREAM (round 6: slot refill and growth
- * without a copy).  Stream b's rows live in 32-position pages: d_page_table[b * table_stride + c] (uint64) is the
+ * without a copy).  Stream b's rows live in 32-position pages: d_page_table[b * table_stride + c] (uint64; the table
+ * 8-byte aligned, so a row range of a larger table is a table too) is the
  * device address (16-byte aligned; 0 = none) of the page holding its stream rows 32c .. 32c + 31, i.e. positions
  * T0 + 32c ...; this layer's block of the page starts `layer_offset` elements after that address and holds
  * [K|V][H][32][D] in the kv_format's element type (K at +0, V at +H*32*D; the pool decides where the layers of a page

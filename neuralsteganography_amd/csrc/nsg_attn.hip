@@ -1043,9 +1043,11 @@ extern "C" int ns_decode_attention_paged(const void* d_qkv, int64_t qkv_stride, 
     const int64_t esz = kv_format == NS_KV_FP8 ? 1 : 2;
     if (T0 > 0 && (!d_k_prefix || !d_v_prefix || prefix_h_stride < (int64_t)T0 * D || ((prefix_h_stride * esz) & 15)))
         return NS_ERR_CONFIG;
-    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_out | (uintptr_t)d_page_table |
-                            (uintptr_t)(T0 > 0 ? d_k_prefix : d_qkv) | (uintptr_t)(T0 > 0 ? d_v_prefix : d_qkv);
-    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || ((uintptr_t)d_lens & 3u)) return NS_ERR_CONFIG;
+    const uintptr_t align = (uintptr_t)d_qkv | (uintptr_t)d_out | (uintptr_t)(T0 > 0 ? d_k_prefix : d_qkv) |
+                            (uintptr_t)(T0 > 0 ? d_v_prefix : d_qkv);
+    if ((align & 15u) || (qkv_stride & 7) || (out_stride & 7) || ((uintptr_t)d_lens & 3u) ||
+        ((uintptr_t)d_page_table & 7u))  // table entries are read one uint64 at a time: any row of a table works
+        return NS_ERR_CONFIG;
     if (qkv_stride < 3LL * H * D || out_stride < (int64_t)H * D) return NS_ERR_CONFIG;
     if ((int64_t)B * H > 0x7FFFFFFF) return NS_ERR_UNSUPPORTED;
     nsg::PagedArgs a;
