@@ -135,8 +135,11 @@ class BatchedGPT2:
         # launches (one half's GEMMs overlap the other's attention); 1 = one launch chain
         self.decode_lanes = 1
         self.decode_lanes_min_batch = 1024
-        self.decode_lanes_order = "alternate"  # or "free": no ordering between the lanes
+        self.decode_lanes_order = "alternate"  # or "free": no ordering between the lanes; "split": attention stream +
+        # GEMM stream
+        self.decode_lane_cu_split = None  # "split": fraction of each XCD's CUs masked to the attention stream
         self._side = None
+        self._split = None
         if self.native:
             from .. import _lib
 
@@ -586,11 +589,13 @@ class BatchedGPT2:
         if len(lanes) == 1:
             self._decode_rows(L, st, tok, out, 0, B, done_ptr, done_stride, stop_ptr)
             return out
+        main = torch.cuda.current_stream(self.device)
+        if self.decode_lanes_order == "split":
+            return self._decode_split(L, main, tok, out, lanes, done_ptr, done_stride, stop_ptr)
         # two lanes (row halves) on two streams, their attention launches alternating (lane 0 layer i, lane 1 layer
         # i, lane 0 layer i + 1, ...): one lane's GEMMs / layer norms run beside the other lane's HBM-bound attention
         # instead of after it.  Rows are independent (batch invariance), so the bits are those of one launch chain.
         side = self._side_stream()
-        main = torch.cuda.current_stream(self.device)
         fork = torch.cuda.Event()
         fork.record(main)
         side.wait_event(fork)
@@ -618,6 +623,48 @@ class BatchedGPT2:
         main.wait_event(join)
         return out
 
+    def _decode_split(self, L, main, tok, out, lanes, done_ptr, done_stride, stop_ptr):
+        """Two lanes, the attention launches on one stream (lane 0 layer i, lane 1 layer i, lane 0 layer i + 1, ...)
+        and every other launch on a second one: lane k's GEMMs of layer i run while lane 1-k's attention of layer i
+        streams.  With ``decode_lane_cu_split`` the two streams are CU-masked (that fraction of every XCD's CUs for the
+        attention stream, the rest for the other), so the GEMMs get CUs while the attention holds the rest."""
+        sa, sg = self._split_streams()
+        fork = torch.cuda.Event()
+        fork.record(main)
+        sg.wait_event(fork)
+        sa.wait_event(fork)
+        gens = [self._decode_rows_gen(L, sg.cuda_stream, tok, out, r, n, done_ptr, done_stride, stop_ptr,
+                                      st_attn=sa.cuda_stream) for r, n in lanes]
+        att = [None, None]  # event after each lane's latest attention launch
+        for _ in range(self.shape.n_layer):
+            for k in (0, 1):
+                if att[k] is not None:
+                    sg.wait_event(att[k])
+                next(gens[k])  # lane k: the launches before its attention (on sg)
+                ev = torch.cuda.Event()
+                ev.record(sg)
+                sa.wait_event(ev)
+                next(gens[k])  # its attention (on sa)
+                att[k] = torch.cuda.Event()
+                att[k].record(sa)
+        for k in (0, 1):
+            sg.wait_event(att[k])
+            for _ in gens[k]:  # the last layer's GEMMs, ln_f and the head
+                pass
+        join = torch.cuda.Event()
+        join.record(sg)
+        main.wait_event(join)
+        return out
+
+    def _split_streams(self):
+        if self._split is None:
+            frac = self.decode_lane_cu_split
+            if frac is None:
+                self._split = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
+            else:
+                self._split = (_cu_masked_stream(self.device, frac, True), _cu_masked_stream(self.device, frac, False))
+        return self._split
+
     def _lanes(self, B: int):
         """Row ranges of the decode step's lanes: one, or two halves (``decode_lanes`` = 2) when B is large enough
         for both halves to fill the chip."""
@@ -642,9 +689,10 @@ class BatchedGPT2:
         for _ in it:
             pass
 
-    def _decode_rows_gen(self, L, st, tok, out, r0, B, done_ptr, done_stride, stop_ptr):
+    def _decode_rows_gen(self, L, st, tok, out, r0, B, done_ptr, done_stride, stop_ptr, st_attn=None):
         from .. import _lib
 
+        st_attn = st if st_attn is None else st_attn
         s = self.shape
         kv = self.kv
         C = s.n_embd
@@ -693,7 +741,8 @@ class BatchedGPT2:
             rc = L.ns_decode_attention_paged(qkv, ldq, table, kv.table.stride(0), kv.width, kv.pool.layer_offset(i),
                                              kp.data_ptr() if T0 else None, vp.data_ptr() if T0 else None,
                                              kp.stride(0) if T0 else 0, T0, B, H, D, lens, self.window,
-                                             self._kv_format, done, done_stride, stop, o, C, 1.0 / math.sqrt(D), st)
+                                             self._kv_format, done, done_stride, stop, o, C, 1.0 / math.sqrt(D),
+                                             st_attn)
             ok(rc, "ns_decode_attention_paged")
             yield  # after it
             gemm(o, C, lw["o_wt"], lw["o_b"], h, C, _lib.NS_LM_EPI_RESIDUAL, C, C)
@@ -776,6 +825,28 @@ class BatchedGPT2:
             h = self._block(i, h, 1, causal=False)
         self.L += 1
         return self._logits(h[:, -1])
+
+
+def _cu_masked_stream(device, frac: float, first: bool):
+    """A HIP stream whose kernels may run on a subset of the CUs (``hipExtStreamCreateWithCUMask``): the first
+    ``frac`` of every 8 consecutive CU ids (``first``) or the rest -- an even share of each XCD whatever way the ids
+    interleave the XCDs.  Eager launches only (a captured graph does not keep a stream's mask)."""
+    import ctypes
+
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    k = max(1, min(7, int(round(8 * float(frac)))))
+    bits = [((i % 8) < k) == first for i in range(ncu)]
+    words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
+    for i, on in enumerate(bits):
+        if on:
+            words[i // 32] |= 1 << (i % 32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), words)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(handle.value, device=device)
 
 
 def _normalise_device(dev: torch.device) -> torch.device:

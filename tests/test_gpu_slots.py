@@ -291,8 +291,8 @@ def test_history_and_table_growth_inside_the_pipelined_loop():
     assert max(map(len, ref)) > 64  # several growths of the 8-token start
 
 
-@pytest.mark.parametrize("order", ["alternate", "free"])
-def test_two_decode_lanes_give_the_same_tokens(order):
+@pytest.mark.parametrize("order,cu_split", [("alternate", None), ("free", None), ("split", None), ("split", 0.5)])
+def test_two_decode_lanes_give_the_same_tokens(order, cu_split):
     """The decode step as two row halves on two streams (``decode_lanes = 2``, one half's GEMMs beside the other's
     attention): the same tokens as one launch chain -- graph-replayed with refilled slots and compaction, eager -- and
     the decode round-trips through the lanes too."""
@@ -302,6 +302,7 @@ def test_two_decode_lanes_give_the_same_tokens(order):
             enumerate([24, 3, 40, 16, 1, 31, 24, 8, 48, 12, 20, 5, 33, 9, 17, 26, 2, 44, 11, 30])]
     ref = lm.encode_batch(bits, ctx, quality=Q)
     lm.lm.decode_lanes, lm.lm.decode_lanes_min_batch, lm.lm.decode_lanes_order = 2, 2, order
+    lm.lm.decode_lane_cu_split = cu_split
     try:
         assert lm.encode_batch(bits, ctx, quality=Q) == ref
         assert lm.encode_batch(bits, ctx, quality=Q, slots=7) == ref

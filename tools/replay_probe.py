@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=0, help="then this many more blocks of --reps replays, timed")
     ap.add_argument("--lanes", type=int, default=1, help="decode-step lanes (BatchedGPT2.decode_lanes)")
     ap.add_argument("--order", default="alternate", help="lane order: alternate | free")
+    ap.add_argument("--cu-split", type=float, default=None, help="split order: CU fraction of the attention stream")
     ap.add_argument("--eager", action="store_true", help="launch every step eagerly instead of replaying the graph")
     args = ap.parse_args()
     import torch
@@ -33,6 +34,7 @@ def main():
     lm = A.HipArithmeticLM(random_gpt2("gpt2", seed=1234), None, logits_dtype="f16", max_batch=B, kv_dtype=args.kv,
                            attention_window=args.window)
     lm.lm.decode_lanes, lm.lm.decode_lanes_order = args.lanes, args.order
+    lm.lm.decode_lane_cu_split = args.cu_split
     q = {"temp": 0.9, "precision": 26, "topk": 300}
     ctx_ids = [lm.vocab - 1] + list(synthetic.DEFAULT_CONTEXT[1:])
     bits = [synthetic.bytes_to_bits_lsb(synthetic.payload_bytes(s, 1024)) for s in range(B)]
@@ -54,7 +56,7 @@ def main():
     for _ in range(args.skip):
         g.replay()
     torch.cuda.synchronize()
-    out = {"batch": B, "lanes": args.lanes, "order": args.order, "eager": args.eager, "kv": args.kv, "window": args.window, "reps": args.reps, "L": lm.lm.L}
+    out = {"batch": B, "lanes": args.lanes, "order": args.order, "cu_split": args.cu_split, "eager": args.eager, "kv": args.kv, "window": args.window, "reps": args.reps, "L": lm.lm.L}
     t0 = time.perf_counter()
     for _ in range(args.reps):
         g.replay()
