@@ -105,6 +105,12 @@ __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d
     return (uint32_t)w;
 }
 
+#ifndef NSG_ATT_DB8
+#define NSG_ATT_DB8 0  // 1: fp8 pages keep the register double buffer in multi-pair workgroups too (A/B)
+#endif
+#ifndef NSG_ATT_DB8_WPE
+#define NSG_ATT_DB8_WPE 3  // ... at this many waves per SIMD
+#endif
 #ifndef NSG_ATT_F8_NI
 #define NSG_ATT_F8_NI 2  // 16-row wave-loads per fp8 chunk
 #endif
@@ -454,7 +460,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {  // lane 
 }
 
 template <class F, int P>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 : 1))) void paged_attn_kernel(
+constexpr int paged_waves_per_eu() {  // NSG_ATT_DB8 fp8: room for the second chunk's registers
+    return P == 1 ? 1 : (NSG_ATT_DB8 && std::is_same<F, FmtF8>::value) ? NSG_ATT_DB8_WPE : 4;
+}
+
+template <class F, int P>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves_per_eu<F, P>()))) void paged_attn_kernel(
     const PagedArgs a) {
     typedef typename F::Elem E;
     typedef typename F::Raw Raw;
@@ -649,7 +660,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
         };
         auto interior = [&](int j0) { return j0 >= T0 && j0 + RPI * NI <= L0; };
         Raw kr[NI], vr[NI];
-        if constexpr (P > 1) {
+        if constexpr (P > 1 && !(NSG_ATT_DB8 && std::is_same<F, FmtF8>::value)) {
             int k = 0;
             for (int j0 = jbeg; j0 < Lend; j0 += step, ++k) {
                 if (interior(j0)) {
@@ -660,7 +671,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P > 1 ? 4 :
                     math_chunk(j0, std::true_type{}, kr, vr);
                 }
             }
-        } else {  // one pair per workgroup (small batches): register double buffer, as the lockstep kernel
+        } else {  // one pair per workgroup (small batches; NSG_ATT_DB8: fp8 always): register double buffer, as the
+                  // lockstep kernel
             Raw kn[NI], vn[NI];
             int j0 = jbeg, k = 0;
             if (j0 < Lend) {

@@ -628,6 +628,8 @@ class BatchedGPT2:
         and every other launch on a second one: lane k's GEMMs of layer i run while lane 1-k's attention of layer i
         streams.  With ``decode_lane_cu_split`` the two streams are CU-masked (that fraction of every XCD's CUs for the
         attention stream, the rest for the other), so the GEMMs get CUs while the attention holds the rest."""
+        if torch.cuda.is_current_stream_capturing():  # measured: the runtime crashes ending such a capture, and a
+            raise RuntimeError("split decode lanes run eagerly only (graphs=False)")  # graph drops the CU masks
         sa, sg = self._split_streams()
         fork = torch.cuda.Event()
         fork.record(main)
@@ -651,9 +653,10 @@ class BatchedGPT2:
             sg.wait_event(att[k])
             for _ in gens[k]:  # the last layer's GEMMs, ln_f and the head
                 pass
-        join = torch.cuda.Event()
-        join.record(sg)
-        main.wait_event(join)
+        for stream in (sg, sa):  # both streams rejoin the caller's directly (a graph capture ends on it)
+            join = torch.cuda.Event()
+            join.record(stream)
+            main.wait_event(join)
         return out
 
     def _split_streams(self):
