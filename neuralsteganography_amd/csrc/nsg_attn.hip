@@ -488,9 +488,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves
             pL0 = a.lens[b];
             const bool skip = (a.done && (a.done[(int64_t)b * a.done_stride] & 1u)) || (a.stop && pL0 >= a.stop[b]);
             if (!skip) {
-                const int jj = pL0 - a.T0;  // the new token's stream row: inside the table (its page is checked by
-                                            // the pair's tasks, one load fewer before the streaming starts)
-                if (jj < 0 || (jj >> 5) >= a.max_chunks) {
+                // the new token's stream row: its page must exist (host invariant).  One pair per workgroup (P = 1,
+                // small batches): checked here, once; multi-pair workgroups: only the row is checked here and the page
+                // by the pair's tasks, one load fewer before their streaming starts (2-3 % at short keys, B = 4,096;
+                // at B = 1 the setup check measured 3-4 % faster per token, profiles/r06/c2_attn_setup_ab.txt)
+                const int jj = pL0 - a.T0;
+                const bool inside = jj >= 0 && (jj >> 5) < a.max_chunks;
+                uint64_t pg = inside ? 1u : 0u;
+                if constexpr (P == 1) pg = inside ? a.table[(int64_t)b * a.tstride + (jj >> 5)] : 0;
+                if (pg == 0 || (P == 1 && (pg & 15u))) {
                     pst = 2;  // no page: poison the output (NaN logits the coder rejects), never write
                 } else {
                     pst = 1;
@@ -549,6 +555,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves
         auto kaddr = [&](uint64_t page, int jj) -> E* { return (E*)page + hoff + (int64_t)(jj & 31) * ATT_D; };
         const E* kpb = (const E*)a.kp + (int64_t)h * a.ph + c * DPL;
         const E* vpb = (const E*)a.vp + (int64_t)h * a.ph + c * DPL;
+        if constexpr (P == 1) {
+            if (g == 0 && wv == 0) {  // KV append of the new token (position L0, page checked in the setup)
+                E* kd = kaddr(trow[(L0 - T0) >> 5], L0 - T0);
+                *(Raw*)kd = knew;
+                *(Raw*)(kd + a.v_off) = vnew;
+            }
+        }
         float m = -1e30f, l = 0.0f;
         float acc[DPL];
 #pragma unroll
@@ -575,22 +588,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves
             pa = readlane64(pgA, k - kbase);
             pb = readlane64(pgB, k - kbase);
         };
-        // the new token's page: a missing one (host invariant broken) poisons the pair -- every one of its tasks
-        // reads the same entry, writes nothing and hands NaN on (S = 1: the output row; S > 1: the partials, which
-        // the merge turns into NaN).  The first iterations' page addresses are requested before it, so both table
-        // reads are in flight together (the prefetch reads entries of cached rows only: inside the table).
-        {
-            uint64_t pa0, pb0;
-            pages_of(0, pa0, pb0);
+        // multi-pair workgroups: the new token's page -- a missing one (host invariant broken) poisons the pair: every
+        // one of its tasks reads the same entry, writes nothing and hands NaN on (S = 1: the output row; S > 1: the
+        // partials, which the merge turns into NaN).  The first iterations' page addresses are requested before it,
+        // so both table reads are in flight together (the prefetch reads entries of cached rows only).
+        bool bad = false;
+        if constexpr (P > 1) {
+            {
+                uint64_t pa0, pb0;
+                pages_of(0, pa0, pb0);
+            }
+            const uint64_t apage = trow[(L0 - T0) >> 5];
+            bad = apage == 0 || (apage & 15u);
+            if (g == 0 && wv == 0 && !bad) {  // KV append of the new token (position L0)
+                E* kd = kaddr(apage, L0 - T0);
+                *(Raw*)kd = knew;
+                *(Raw*)(kd + a.v_off) = vnew;
+            }
         }
-        const uint64_t apage = trow[(L0 - T0) >> 5];
-        const bool bad = apage == 0 || (apage & 15u);
         const int Lend = bad ? 0 : Lk;  // the streaming loops run while j0 < Lend
-        if (g == 0 && wv == 0 && !bad) {  // KV append of the new token (position L0)
-            E* kd = kaddr(apage, L0 - T0);
-            *(Raw*)kd = knew;
-            *(Raw*)(kd + a.v_off) = vnew;
-        }
         // one iteration = RPI*NI = 32 consecutive rows from j0; GENERAL handles the prefix boundary, the clamp past
         // the cache and the new token; an interior run (stream rows < L0 only) spans at most two pages
         auto load_chunk = [&](int j0, int k, auto general, Raw (&kr)[NI], Raw (&vr)[NI]) {
