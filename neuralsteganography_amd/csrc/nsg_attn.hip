@@ -453,6 +453,27 @@ struct PagedArgs {
     float scale_log2;
 };
 
+#ifndef NSG_ATT_DPP
+#define NSG_ATT_DPP 1  // paged kernel: the score sums over a row's LPR lanes by DPP moves instead of ds_bpermute (a
+                       // DPP lane ^ 8 step in the final row-group merge spilled 7-18 VGPRs at P = 8: not used)
+#endif
+
+// x + (x of lane l ^ 1), then + (lane ^ 2), then (LPR = 8) + the other quad's sum -- the xor butterfly's values in
+// its order (the third step reads lane 7 - l, whose quad sum equals lane l ^ 4's), as VALU DPP moves instead of
+// LDS permutes: the same bits as __shfl_xor's butterfly
+template <int LPR>
+__device__ __forceinline__ float row_group_sum(float x) {
+    static_assert(LPR == 4 || LPR == 8, "rows of 4 or 8 lanes");
+    auto dpp = [](float v, auto ctrl) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                     decltype(ctrl)::value, 0xF, 0xF, false));
+    };
+    x += dpp(x, std::integral_constant<int, 0xB1>{});  // quad_perm [1,0,3,2]: lane ^ 1
+    x += dpp(x, std::integral_constant<int, 0x4E>{});  // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (LPR == 8) x += dpp(x, std::integral_constant<int, 0x141>{});  // row_half_mirror: lane 7 - l
+    return x;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {  // lane uniform: the value lands in SGPRs
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
@@ -654,8 +675,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves
                     vr[u] = vnew;
                 }
                 float sv = F::dot(q, kr[u]);
+                if constexpr (NSG_ATT_DPP) {
+                    sv = row_group_sum<LPR>(sv);
+                } else {
 #pragma unroll
-                for (int off = 1; off < LPR; off <<= 1) sv += __shfl_xor(sv, off);
+                    for (int off = 1; off < LPR; off <<= 1) sv += __shfl_xor(sv, off);
+                }
                 sc[u] = sv * a.scale_log2;
                 if (valid[u]) mx = fmaxf(mx, sc[u]);
             }

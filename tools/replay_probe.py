@@ -46,13 +46,19 @@ def main():
     if not lm.lm.reserve(args.skip + args.reps * (2 + args.blocks) + 8):  # the paged cache: map every page ahead
         raise SystemExit("no device memory for the pages")
     sess = coder_mod.EncodeSession(ctx, bits, max_tokens=budget)
-    g = A._StepGraph(lm.lm, lambda lg: sess.step(lg), logits)
-    if args.eager:
-        def eager():
-            g._body()
-            g.lm.L += 1
+    if args.eager:  # no graph at all (a captured graph does not keep CU-masked streams)
+        import types
 
-        g.replay = eager
+        buf = logits.clone()
+        lm.lm.begin_static(buf)
+
+        def eager():
+            lm.lm.step_static(sess.step(buf))
+            lm.lm.L += 1
+
+        g = types.SimpleNamespace(replay=eager)
+    else:
+        g = A._StepGraph(lm.lm, lambda lg: sess.step(lg), logits)
     for _ in range(args.skip):
         g.replay()
     torch.cuda.synchronize()
