@@ -454,8 +454,8 @@ struct PagedArgs {
 };
 
 #ifndef NSG_ATT_DPP
-#define NSG_ATT_DPP 1  // paged kernel: the score sums over a row's LPR lanes by DPP moves instead of ds_bpermute (a
-                       // DPP lane ^ 8 step in the final row-group merge spilled 7-18 VGPRs at P = 8: not used)
+#define NSG_ATT_DPP 1  // paged kernel: the score sums over a row's LPR lanes and the lane ^ 8 step of the final
+                       // row-group merge by DPP moves instead of ds_bpermute
 #endif
 
 // x + (x of lane l ^ 1), then + (lane ^ 2), then (LPR = 8) + the other quad's sum -- the xor butterfly's values in
@@ -472,6 +472,10 @@ __device__ __forceinline__ float row_group_sum(float x) {
     x += dpp(x, std::integral_constant<int, 0x4E>{});  // quad_perm [2,3,0,1]: lane ^ 2
     if constexpr (LPR == 8) x += dpp(x, std::integral_constant<int, 0x141>{});  // row_half_mirror: lane 7 - l
     return x;
+}
+
+__device__ __forceinline__ float row_ror8(float x) {  // the value of lane l ^ 8 (DPP row_ror:8 in a 16-lane row)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {  // lane uniform: the value lands in SGPRs
@@ -741,16 +745,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(paged_waves
                 }
             }
         }
+        // merge the row groups (lanes c, c + LPR, ... hold the same dims); the lane ^ 8 step as a DPP row_ror:8
+        // (within a 16-lane row that IS lane ^ 8; the merge is symmetric in the two lanes, so the same bits), the
+        // others through ds_bpermute
 #pragma unroll
-        for (int off = LPR; off < 64; off <<= 1) {  // merge the row groups (lanes c, c + LPR, ... hold the same dims)
-            const float mo = __shfl_xor(m, off);
-            const float lo = __shfl_xor(l, off);
+        for (int off = LPR; off < 64; off <<= 1) {
+            const bool dpp8 = NSG_ATT_DPP && off == 8;
+            const float mo = dpp8 ? row_ror8(m) : __shfl_xor(m, off);
+            const float lo = dpp8 ? row_ror8(l) : __shfl_xor(l, off);
             const float mn = fmaxf(m, mo);
             const float fa = exp2f(m - mn), fo = exp2f(mo - mn);
             l = l * fa + lo * fo;
 #pragma unroll
             for (int d = 0; d < DPL; ++d) {
-                const float ao = __shfl_xor(acc[d], off);
+                const float ao = dpp8 ? row_ror8(acc[d]) : __shfl_xor(acc[d], off);
                 acc[d] = acc[d] * fa + ao * fo;
             }
             m = mn;

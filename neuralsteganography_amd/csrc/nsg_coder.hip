@@ -1701,7 +1701,7 @@ static bool launch(ns_ctx* ctx, const nsg::StepParams& p, hipStream_t s) {
 
 extern "C" {
 
-const char* ns_version(void) { return "nsgcoder 0.24 gfx950"; }
+const char* ns_version(void) { return "nsgcoder 0.25 gfx950"; }
 
 int ns_set_split_max_batch(int max_batch) {
     const int prev = split_setting();
